@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/sec of the batched 4v4 littoral env step on MI355X.
+
+Driver contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under
+torch.distributed.run, one process per GPU). Prints ONE JSON line on rank 0.
+
+Workload (BASELINE.json metric/configs): 65 536 parallel 4v4 environments per
+GPU on the 100x100 Baltic grid, reference spawns (blue game.py:556; red
+(98,48),(98,52),(98,56),(96,52)), 40-step episodes with in-kernel auto-reset,
+U[0,1)^4 float32 actions from Philox (seed 42), tactics aggressive, side blue,
+trained red. Envs shard across GPUs by global id (weak scaling, no collective
+on the step path). A "step" = one Game.step over every env of the GPU; inputs
+(actions for all timed steps) are resident in HBM before the timed region.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "littoral-naval-warfare-marl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+REF_BLUE = [(6, 61), (10, 81), (8, 70), (11, 58)]
+REF_RED = [(98, 48), (98, 52), (98, 56), (96, 52)]
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(nb, nr):
+    """Minimum HBM bytes one env-step must move:
+    actions in (f32), observations + rewards + done + cog out, and the SoA state
+    read and written once (26 B/agent + 52 B/env)."""
+    A = nb + nr
+    act = A * 4 * 4
+    obs = (nb * (4 * nb + 52) + nr * (4 * nr + 52)) * 4
+    out = A * 4 + 4 + 4
+    state = A * 26 + 52
+    return act + obs + out + 2 * state
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--envs", type=int, default=65536, help="environments per GPU")
+    p.add_argument("--spawns", choices=["reference", "melee"], default="reference")
+    p.add_argument("--los-mode", type=int, default=0, help="0 LOS table, 1 ray march")
+    p.add_argument("--move-mode", type=int, default=0, help="0 move table, 1 direct A*")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--secondary", action="store_true",
+                   help="also time melee spawns and the march/A* variants (stderr + JSON)")
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_game(E, rank, args, spawns, los_mode, move_mode):
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=True,
+                  auto_reset=True, episode_steps=40, los_mode=los_mode, move_mode=move_mode)
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, device=torch.cuda.current_device(),
+                    env_id_base=rank * E, seed=1234)
+    box = ((40, 40), (57, 65)) if spawns == "melee" else None
+    g.reset(positions=REF_BLUE + REF_RED, box=box)
+    return g
+
+
+def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmup):
+    from lnw import _abi
+    L = _abi.load()
+    g = make_game(E, rank, args, spawns, los_mode, move_mode)
+    A = g.A
+    # inputs resident before the timed region: actions for every step
+    acts = torch.empty((warmup + steps, E, A, 4), dtype=torch.float32, device="cuda")
+    per = E * A * 4
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for s in range(warmup + steps):
+        off = ((rank * (warmup + steps) + s) * per + 3) // 4 * 4
+        _abi.check(L.lnw_fill_uniform_f32(ctypes.c_void_p(acts[s].data_ptr()), per, 42, off, stream))
+    torch.cuda.synchronize()
+    for s in range(warmup):
+        g.step(acts[s])
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        ev[s][0].record()
+        g.step(acts[warmup + s])
+        ev[s][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kms = [a.elapsed_time(b) for a, b in ev]
+    st = g.env_state()
+    err = int((st["err"] != 0).sum())
+    episodes = int(st["episode"].sum())
+    g.close()
+    del acts
+    return elapsed, float(np.mean(kms)), float(np.median(kms)), err, episodes
+
+
+def cpu_baseline(seconds):
+    """The CPU oracle (oracle/lnw_oracle.c, a C restatement of the reference
+    step) timed on one host core over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    L = _oracle.lib()
+    L.orc_bench.restype = ctypes.c_int64
+    L.orc_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                            ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+    from lnw.batched import default_grid
+    grid = np.ascontiguousarray(default_grid(100), np.uint8)
+    P = _oracle.OrcParams(0, 0, 1, 1, 1, 0.4, 74, 70, 14, 82)
+    types = np.array([0] * 4 + [1] * 4, np.int32)
+    pos = np.array(REF_BLUE + REF_RED, np.int32).reshape(-1)
+
+    def run(n_envs, n_steps):
+        t = time.perf_counter()
+        n = L.orc_bench(ctypes.byref(P), grid.ctypes.data_as(ctypes.c_void_p), 100, 4, 4,
+                        types.ctypes.data_as(ctypes.c_void_p), pos.ctypes.data_as(ctypes.c_void_p),
+                        n_envs, n_steps, 40, 42)
+        return n, time.perf_counter() - t
+
+    n, dt = run(16, 40)
+    envs = max(16, int(16 * seconds / max(dt, 1e-3)))
+    n, dt = run(envs, 40)
+    return dict(value=n / dt, unit="env-steps/sec", cores=1, kind="port",
+                sample=f"{envs} envs x 40 steps (4v4, reference spawns, U[0,1) f32 actions, "
+                       f"auto-reset), CPU oracle restatement single-threaded, {dt:.1f} s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    E = args.envs
+    elapsed, kms_mean, kms_med, err, episodes = run_workload(
+        E, rank, world, args, args.spawns, args.los_mode, args.move_mode, args.steps, args.warmup)
+    t = torch.tensor([elapsed, kms_mean], dtype=torch.float64, device="cuda")
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed, kms_mean = float(t[0]), float(t[1])
+    value = world * E * args.steps / elapsed
+    nb = nr = 4
+    B = algorithmic_bytes(nb, nr)
+    achieved = B * E / (kms_mean * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tf):
+        try:
+            tj = json.load(open(tf))
+            key = f"{args.spawns}_e{E}_los{args.los_mode}_mv{args.move_mode}"
+            traffic = tj.get(key)
+        except Exception:
+            traffic = None
+    secondary = {}
+    if args.secondary and rank == 0:
+        for name, sp, lm, mm in (("melee", "melee", 0, 0), ("reference_march_astar", "reference", 1, 1),
+                                 ("melee_march_astar", "melee", 1, 1)):
+            el, km, _, er, _ = run_workload(E, rank, 1, args, sp, lm, mm, args.steps, args.warmup)
+            secondary[name] = dict(env_steps_per_sec=E * args.steps / el, ms_per_step=km, err_envs=er)
+            log(name, secondary[name])
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (whole node), 65536 parallel 4v4 envs on 100x100 grid",
+            "value": value,
+            "unit": "env-steps/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64+i32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{E} parallel 4v4 envs per GPU, 100x100 Baltic grid, "
+                            f"{args.spawns} spawns, 40-step episodes with auto-reset, "
+                            "U[0,1)^4 f32 actions",
+                "envs_per_gpu": E, "global_envs": world * E, "agents": "4v4",
+                "grid": 100, "spawns": args.spawns, "los_mode": args.los_mode,
+                "move_mode": args.move_mode, "parallelism": f"env-shard x{world}",
+            },
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_env_step": B,
+                         "kernel_ms_mean": kms_mean, "kernel_ms_median": kms_med},
+            "cpu_baseline": cpu,
+            "err_envs": err,
+            "episodes_completed": episodes,
+        }
+        if secondary:
+            line["secondary"] = secondary
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

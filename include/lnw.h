@@ -1,0 +1,220 @@
+/*
+ * lnw.h — C-ABI of the MI355X-native batched littoral-warfare environment step.
+ *
+ * Drop-in boundary for the reference's environment API
+ * (valauri/Littoral-Naval-Warfare-MARL):
+ *
+ *   lnw_create / lnw_load_terrain   replace Game.__init__ (game.py:107-158) and
+ *                                   Game.define_grid_from_image (game.py:616-626)
+ *   lnw_reset                       replaces Game.reset (game.py:528-613)
+ *   lnw_step                        replaces Game.step (game.py:298-525) with
+ *                                   Combatant/LandingShip.take_action
+ *                                   (combatant.py:501-565, landingship.py:508-572)
+ *                                   and Game.calculate_reward (game.py:214-295)
+ *   lnw_observe                     replaces ship.get_obs() (combatant.py:90-233,
+ *                                   landingship.py:94-239) as called by
+ *                                   main.py:282, ppo.py:500, ddqn.py:296
+ *   lnw_los_batch                   check_line_of_sight (combatant.py:436-456)
+ *   lnw_move_batch                  continuous_to_discrete / value_to_coordinates +
+ *                                   check_path / astar (combatant.py:289-489,689-704)
+ *
+ * Conventions
+ *  - Every pointer argument named *_dev is a device pointer (HIP, gfx950); the
+ *    caller owns action/observation/reward buffers, the handle owns the
+ *    environment state and the terrain.
+ *  - Work is enqueued on the caller's stream (hipStream_t passed as void*; NULL
+ *    = the default stream). Nothing synchronises except lnw_create,
+ *    lnw_load_terrain and lnw_destroy.
+ *  - Every function returns 0 on success or a negative LNW_E* code; the message
+ *    of the last failure on the calling thread is available from
+ *    lnw_last_error(). Reference crash modes (ZeroDivisionError in an EW fix,
+ *    round(nan), tape exhaustion) do not abort: they set per-environment bits in
+ *    the err-flags array (LNW_ERRF_*).
+ *  - A handle is not thread-safe; use one handle per device (per process).
+ *
+ * Layouts (E = n_envs, nb/nr = blue/red slots, A = nb+nr, D_side = 4*n_side+52):
+ *  actions   [E][A][4]  f32 or f64 (continuous), or [E][A][4] i32 (discrete:
+ *                       radar, salvo, move-index 0..49, unused) — mutated in
+ *                       place where the reference mutates it (game.py:379)
+ *  obs_blue  [E][nb][Db] f32, obs_red [E][nr][Dr] f32 (float32 of the reference's
+ *                       float64 value; dead slots are zeros)
+ *  rew_blue  [E][nb] f32, rew_red [E][nr] f32, done [E] i32 (1 running, 0 over),
+ *  cog       [E] f32 (NaN where the reference returns None)
+ */
+#ifndef LNW_H
+#define LNW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LNW_ABI_VERSION 1
+
+/* status codes */
+#define LNW_OK 0
+#define LNW_EINVAL (-1)
+#define LNW_ENOMEM (-2)
+#define LNW_EDEVICE (-3)
+#define LNW_ESTATE (-4)
+#define LNW_EUNSUPPORTED (-5)
+
+/* ship types (Combatant "small"/"large", LandingShip "ls") */
+#define LNW_SMALL 0
+#define LNW_LARGE 1
+#define LNW_LS 2
+
+/* action dtypes / per-row value kinds (NumPy NEP 50 semantics) */
+#define LNW_ACT_F32 0      /* whole buffer float32 (np.float32 rows)            */
+#define LNW_ACT_F64 1      /* whole buffer float64 (np.float64 rows)            */
+#define LNW_ACT_I32 2      /* discrete integer actions (DISCRETE=true)         */
+#define LNW_KIND_PYFLOAT 1 /* row_kind values for an F64 buffer: python floats */
+#define LNW_KIND_F32 2     /*   np.float32 row stored widened to f64           */
+#define LNW_KIND_F64 3     /*   np.float64 row                                 */
+
+/* rng modes */
+#define LNW_RNG_PHILOX 0   /* production: Philox4x32-10 keyed by (seed, global env id) */
+#define LNW_RNG_TAPE 1     /* parity: per-env recorded draws                           */
+
+/* per-env error bits */
+#define LNW_ERRF_ZERODIV 1u    /* combatant.py:274 ZeroDivisionError (fix skipped) */
+#define LNW_ERRF_NAN_ROUND 2u  /* round(nan/inf) in a fix or a radar action        */
+#define LNW_ERRF_TAPE 4u       /* tape exhausted                                   */
+#define LNW_ERRF_MISSILES 8u   /* missile count outside the 0..8 hit table         */
+
+/* observe selectors */
+#define LNW_OBS_ALL (-1)   /* every live ship, blue then red (main.py:280-333) */
+#define LNW_OBS_BLUE (-2)
+#define LNW_OBS_RED (-3)
+
+typedef struct lnw_handle lnw_handle;
+
+/* Scenario flags: the reference's config.json keys (game.py:41-53,
+ * combatant.py:33-38) that change step semantics. */
+typedef struct lnw_params {
+    int32_t discrete;        /* overall.discrete                       */
+    int32_t landing_ops;     /* overall.landing_ops                    */
+    int32_t aggressive;      /* overall.tactics == "aggressive"        */
+    int32_t side_blue;       /* environment_setup.side == "blue"       */
+    int32_t trained_red;     /* environment_setup.trained_red          */
+    int32_t move_thr;        /* environment_setup.movement_threshold   */
+    int32_t ew_thr;          /* environment_setup.ew_threshold         */
+    int32_t lz_x, lz_y;      /* landing zone (game.py:590): (14, 82)   */
+    double red_aggression;   /* environment_setup.red_aggression       */
+    /* build-side knobs (not in the reference) */
+    int32_t episode_steps;   /* auto-reset horizon (0 = never)          */
+    int32_t auto_reset;      /* reset an env in-kernel when done==0 or at the horizon */
+    int32_t los_mode;        /* 0 = precomputed LOS table, 1 = ray march   */
+    int32_t move_mode;       /* 0 = precomputed move table, 1 = direct A*  */
+} lnw_params;
+
+/* Spawn description used by lnw_reset and by in-kernel auto-reset.
+ * types[A]: LNW_SMALL/LARGE/LS; pos[A][2]: spawn cell; rand_ls[A] != 0 draws the
+ * cell with random.randint(98,99), random.randint(48,56) (game.py:589).
+ * If box_lo/box_hi are set (box_hi[0] > box_lo[0]) every agent instead spawns on
+ * a random water cell of that box (a build-side "melee" scenario, drawn from a
+ * separate Philox stream so the game stream is unchanged). */
+typedef struct lnw_spawn {
+    int32_t types[64];
+    int32_t pos[64][2];
+    int32_t rand_ls[64];
+    int32_t box_lo[2], box_hi[2];
+} lnw_spawn;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int lnw_abi_version(void);
+const char *lnw_last_error(void);
+
+/* env_id_base: global id of this handle's first env (multi-GPU sharding keys the
+ * RNG by global env id so trajectories do not depend on the GPU count). */
+int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr, int32_t device,
+               int64_t env_id_base, lnw_handle **out);
+int lnw_destroy(lnw_handle *h);
+
+/* Upload the uint8 terrain (row-major [G][G], grid[x][y]) and build the device
+ * structures: radar/EW bitmask, move-feasibility table, LOS table. Synchronous. */
+int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G);
+
+int lnw_set_rng(lnw_handle *h, int32_t mode, uint64_t seed, const double *tape_dev,
+                const int64_t *tape_off_dev);
+
+/* ---- environment API ---------------------------------------------------- */
+/* env_mask_dev: [E] u8, nonzero = reset that env (NULL = all).
+ * pos_dev: optional [E][A][2] i32 per-env spawn cells (overrides spawn->pos). */
+int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn,
+              const int32_t *pos_dev, void *stream);
+
+int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
+             float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
+             int32_t *done_dev, float *cog_dev, void *stream);
+
+/* agent >= 0: that agent (blue 0..nb-1, red nb..A-1) in every env;
+ * LNW_OBS_ALL / LNW_OBS_BLUE / LNW_OBS_RED: every live ship of the selection,
+ * in list order. Side effects as the reference (target lists, RNG draws). */
+int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_red_dev,
+                void *stream);
+
+/* ---- state access (tests, facade, checkpoint) --------------------------- */
+#define LNW_F_POS 0        /* [A][E] u32: x | y<<16                          */
+#define LNW_F_RADAR 1      /* [A][E] i32                                     */
+#define LNW_F_MISSILES 2   /* [A][E] u8  missile count                       */
+#define LNW_F_MKIND 3      /* [A][E] u8  value kind of the missile count     */
+#define LNW_F_ALIVE 4      /* [A][E] u8  list slot is not None               */
+#define LNW_F_TYPE 5       /* [A][E] u8                                      */
+#define LNW_F_STEPS 6      /* [A][E] i32 ship.steps_done                     */
+#define LNW_F_DIST_LZ 7    /* [A][E] f64 LandingShip.distance_to_landing_zone */
+#define LNW_F_TL_CNT 8     /* [A][E] u16 len(target_list)                    */
+#define LNW_F_TL 9         /* [A][T][E] u16 x | y<<8                         */
+#define LNW_F_DUCT 10      /* [E] f64                                        */
+#define LNW_F_ENV 11       /* [8][E] i32: n_blue_left, n_red_left, steps_done,
+                              blue_victory, red_victory, blue_engagements,
+                              red_engagements, episode                      */
+#define LNW_F_RNG 12       /* [E] u64 Philox counter or tape cursor          */
+#define LNW_F_ERR 13       /* [E] u32 LNW_ERRF_* bits                        */
+#define LNW_NFIELDS 14
+
+/* Device pointer and byte size of one state field (valid until lnw_destroy). */
+int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbytes);
+/* Target-list capacity T per agent (= max(nb,nr) + max(nb,nr)^2, never overflows). */
+int lnw_tlist_cap(lnw_handle *h);
+
+/* ---- unit kernels (parity tests, standalone use) ------------------------ */
+/* LOS (radar thr = move_thr; EW thr): out[i] = bit0 radar clear | bit1 EW clear
+ * for pairs[i] = (x1, y1, x2, y2), traced from (x1,y1) to (x2,y2). */
+int lnw_los_batch(const uint8_t *grid_dev, int32_t G, const int16_t *pairs_dev, int64_t n,
+                  int32_t move_thr, int32_t ew_thr, uint8_t *out_dev, void *stream);
+/* A*: plen[i] (-1 = None), kind[i] (0 goal, 1 timeout, 2 none), feasible[i]
+ * (check_path) for ship type types[i] from start[i] to target[i]. */
+int lnw_astar_batch(const uint8_t *grid_dev, int32_t G, int32_t move_thr, const int8_t *types_dev,
+                    const int16_t *start_dev, const int16_t *target_dev, int64_t n,
+                    int16_t *plen_dev, int8_t *kind_dev, uint8_t *feasible_dev, void *stream);
+/* Continuous move target: rounded (x,y) and feasibility (can_move_to && check_path)
+ * through the handle's structures (table or direct A* per params.move_mode). */
+int lnw_move_batch(lnw_handle *h, const int8_t *types_dev, const int16_t *pos_dev,
+                   const double *act_dev /* [n][2] */, const uint8_t *is_f32_dev, int64_t n,
+                   int32_t *rounded_dev, uint8_t *ok_dev, void *stream);
+/* check_path(start, target) through the handle's move table (params.move_mode 0,
+ * targets within +-4) or the A* replica. start must lie inside the grid. */
+int lnw_path_query(lnw_handle *h, const int8_t *types_dev, const int16_t *start_dev,
+                   const int16_t *target_dev, int64_t n, uint8_t *out_dev, void *stream);
+/* The handle's LOS query (table or march per params.los_mode). */
+int lnw_los_query(lnw_handle *h, const int16_t *pairs_dev, int64_t n, uint8_t *out_dev,
+                  void *stream);
+
+/* Stream-ordered byte copy (device<->device/host), for state access. */
+int lnw_copy(void *dst, const void *src, int64_t nbytes, void *stream);
+
+/* Philox U[0,1) float32 fill keyed by (seed, offset + i): synthetic actions. */
+int lnw_fill_uniform_f32(float *out_dev, int64_t n, uint64_t seed, uint64_t offset,
+                         void *stream);
+
+/* Host-side constants the kernels use (for tests): hit probability tables
+ * 1-(1-p)^n for p in {0.45, 0.63}, n = 0..8, in float64 and float32. */
+int lnw_hit_tables(double *tab64 /* [2][9] */, float *tab32 /* [2][9] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LNW_H */

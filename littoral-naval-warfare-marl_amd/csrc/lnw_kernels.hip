@@ -1,0 +1,1505 @@
+// lnw_kernels.hip — MI355X (gfx950) kernels and C-ABI of the batched littoral
+// environment step. See include/lnw.h for the boundary and DESIGN.md for the
+// layout/roofline discussion.
+//
+// Step structure (one 64-lane wavefront = one workgroup = 64 environments):
+//   L  coalesced load of the agent-major SoA state into padded LDS columns
+//   M  movement feasibility for every (env, agent): move target in the row's
+//      value kind, then the precomputed A* table (or the A* replica)
+//   S  the reference's sequential agent loop per env (one lane per env):
+//      firing over the previous target list, radar, commit move, get_obs
+//      (LOS table / ray march, EW bearings + fixes), reward; then the team tail
+//   O  observations written cooperatively: lanes cover consecutive floats of
+//      the [E][n][D] output (256-B coalesced stores), values read from LDS
+//   W  coalesced store of the state (or of an in-kernel auto-reset)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lnw.h"
+#include "lnw_device.h"
+
+using namespace lnw;
+
+namespace {
+
+constexpr int PAD = WAVE + 1;   // padded LDS column stride (words) -> no bank conflicts
+constexpr int PADB = WAVE + 4;  // byte-array stride
+
+// ---------------------------------------------------------------------------
+// per-wave LDS carve-up for the step/observe kernels
+// ---------------------------------------------------------------------------
+struct LdsLayout {
+  int pos_cur, pos_old, pos_new, radar_cur, radar_old, reward;        // word/dword offsets (bytes)
+  int miss_cur, miss_old, mkind, type, alive0, eng, tcnt, obsd;       // byte arrays
+  int observed, bcnt, border, open, mask, total;
+};
+
+__host__ __device__ inline LdsLayout lds_layout(int A, int nmax, int mask_words) {
+  LdsLayout L;
+  int o = 0;
+  L.pos_cur = o; o += A * PAD * 4;
+  L.pos_old = o; o += A * PAD * 4;
+  L.pos_new = o; o += A * PAD * 4;
+  L.radar_cur = o; o += A * PAD * 4;
+  L.radar_old = o; o += A * PAD * 4;
+  o = (o + 7) & ~7;
+  L.reward = o; o += A * PAD * 8;
+  L.tcnt = o; o += A * PAD * 4;
+  L.observed = o; o += nmax * PAD * 4;
+  L.open = o; o += OPEN_CAP * WAVE * 4;
+  L.miss_cur = o; o += A * PADB;
+  L.miss_old = o; o += A * PADB;
+  L.mkind = o; o += A * PADB;
+  L.type = o; o += A * PADB;
+  L.alive0 = o; o += A * PADB;
+  L.eng = o; o += A * PADB;
+  L.obsd = o; o += A * PADB;
+  L.bcnt = o; o += nmax * PADB;
+  L.border = o; o += nmax * PADB;
+  o = (o + 15) & ~15;
+  L.mask = o; o += mask_words * 4;
+  L.total = o;
+  return L;
+}
+
+struct Cols {
+  uint32_t *pos_cur, *pos_old, *pos_new, *tcnt, *observed, *open;
+  int32_t *radar_cur, *radar_old;
+  double *reward;
+  uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border;
+  uint32_t *mask;
+};
+
+__device__ inline Cols carve(char *base, const LdsLayout &L) {
+  Cols c;
+  c.pos_cur = (uint32_t *)(base + L.pos_cur);
+  c.pos_old = (uint32_t *)(base + L.pos_old);
+  c.pos_new = (uint32_t *)(base + L.pos_new);
+  c.radar_cur = (int32_t *)(base + L.radar_cur);
+  c.radar_old = (int32_t *)(base + L.radar_old);
+  c.reward = (double *)(base + L.reward);
+  c.tcnt = (uint32_t *)(base + L.tcnt);
+  c.observed = (uint32_t *)(base + L.observed);
+  c.open = (uint32_t *)(base + L.open);
+  c.miss_cur = (uint8_t *)(base + L.miss_cur);
+  c.miss_old = (uint8_t *)(base + L.miss_old);
+  c.mkind = (uint8_t *)(base + L.mkind);
+  c.type = (uint8_t *)(base + L.type);
+  c.alive0 = (uint8_t *)(base + L.alive0);
+  c.eng = (uint8_t *)(base + L.eng);
+  c.obsd = (uint8_t *)(base + L.obsd);
+  c.bcnt = (uint8_t *)(base + L.bcnt);
+  c.border = (uint8_t *)(base + L.border);
+  c.mask = (uint32_t *)(base + L.mask);
+  return c;
+}
+
+#define COLW(arr, a) ((arr)[(a) * PAD + lane])
+#define COLB(arr, a) ((arr)[(a) * PADB + lane])
+
+// Per-lane (per-env) context for phase S.
+struct Ctx {
+  const KParams &P;
+  const KState &S;
+  Cols &c;
+  int lane, env;
+  double duct;
+  Rng rng;
+  const uint32_t *mask;  // LDS (march mode) or global
+  long long E;
+};
+
+__device__ inline int floordiv7(int v) { int q = v / 7; if ((v % 7 != 0) && (v < 0)) q--; return q; }
+__device__ inline int pymod7(int v) { int m = v % 7; if (m < 0) m += 7; return m; }
+
+// ---------------------------------------------------------------------------
+// movement feasibility (combatant.py:459-489, 382-408, 689-704)
+// ---------------------------------------------------------------------------
+__device__ inline bool check_path_h(const KParams &P, const KState &S, int type, int sx, int sy,
+                                    int tx, int ty, uint32_t *open, int ost) {
+  if (tx < 0 || tx > 99 || ty < 0 || ty > 99) return false;
+  int ox = tx - sx, oy = ty - sy;
+  if (P.move_mode == 0 && ox >= -R_MV && ox <= R_MV && oy >= -R_MV && oy <= R_MV) {
+    int cls = type == T_LS ? 1 : 0;
+    int bit = (ox + R_MV) * MV_W + (oy + R_MV);
+    uint32_t w = S.mvtab[((size_t)cls * P.G * P.G + (size_t)sx * P.G + sy) * MV_WORDS + (bit >> 5)];
+    return (w >> (bit & 31)) & 1u;
+  }
+  MaskBlocked mb{S.mask2, P.W16};
+  bool sb = mb(sx, sy);
+  return check_path_dev(mb, sb, P.G, type, sx, sy, tx, ty, open, ost);
+}
+
+__device__ inline bool can_move_to_h(const KParams &P, const KState &S, int x, int y) {
+  if (0 <= x && x < 100 && 0 <= y && y < 100) return !(cell_bits(S.mask2, P.W16, x, y) & 1u);
+  return false;
+}
+
+// LOS query: table lookup inside the +-40 window, otherwise the ray march
+__device__ inline uint32_t los_q(const KParams &P, const KState &S, const uint32_t *mask, int x1,
+                                 int y1, int x2, int y2) {
+  int dx = x2 - x1, dy = y2 - y1;
+  if (P.los_mode == 0 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS) {
+    int col = (dy + R_LOS) * 2;
+    uint32_t w = S.lostab[((size_t)x1 * P.G + y1) * LOS_CELL_WORDS + (dx + R_LOS) * LOS_ROW_WORDS +
+                          (col >> 5)];
+    return (w >> (col & 31)) & 3u;
+  }
+  return los_march<true>(mask, P.W16, x1, y1, x2, y2);
+}
+
+// ---------------------------------------------------------------------------
+// get_obs sensor fusion (combatant.py:90-161 / landingship.py:94-165): refreshes
+// the target list of agent `me`. Observation floats are written in phase O.
+// ---------------------------------------------------------------------------
+__device__ void get_obs_dev(Ctx &X, int me) {
+  const KParams &P = X.P;
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const long long E = X.E;
+  const int env = X.env;
+  const int nb = P.nb, A = P.A;
+  const int side = me >= nb;
+  const int own0 = side ? nb : 0, own1 = side ? A : nb;
+  const int opp0 = side ? 0 : nb, opp1 = side ? nb : A;
+  const int nopp = opp1 - opp0;
+  const int myradar = COLW(c.radar_cur, me);
+  int obs_n = 0;
+  int norder = 0;
+  for (int q = 0; q < nopp; q++) COLB(c.bcnt, q) = 0;
+
+  for (int i = own0; i < own1; i++) {
+    if (!COLB(c.alive0, i)) continue;
+    uint32_t pi = COLW(c.pos_cur, i);
+    int xi = pos_x(pi), yi = pos_y(pi);
+    int ti = COLB(c.type, i);
+    for (int j = opp0; j < opp1; j++) {
+      if (!COLB(c.alive0, j)) continue;
+      uint32_t pj = COLW(c.pos_cur, j);
+      int xj = pos_x(pj), yj = pos_y(pj);
+      int tj = COLB(c.type, j);
+      int dx = xj - xi, dy = yj - yi;
+      int d2 = dx * dx + dy * dy;
+      int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
+      bool rad_ok = myradar == 1 && d2 < rr * rr;
+      bool close = d2 < 16;
+      bool ew_cand = d2 < re * re && COLW(c.radar_cur, j) == 1;
+      if (!(rad_ok || close || ew_cand)) continue;  // LOS result would be unused
+      uint32_t los = los_q(P, S, X.mask, xi, yi, xj, yj);
+      if (!(los & 1u)) continue;
+      uint32_t pk = pj & 0x7fff7fffu;
+      bool seen = false;
+      for (int q = 0; q < obs_n; q++) seen |= COLW(c.observed, q) == pk;
+      if ((rad_ok || close) && !seen) {
+        COLW(c.observed, obs_n) = pk;
+        obs_n++;
+        seen = true;
+      }
+      if (ew_cand && (los & 2u) && !seen) {
+        // calculate_bearing (combatant.py:249-263)
+        double bearing = atan2((double)dy, (double)dx) * RAD2DEG;
+        double distortion = X.rng.gauss();
+        if (bearing + distortion < 0)
+          bearing = bearing + distortion + 360.0;
+        else
+          bearing = bearing + distortion;
+        int jj = j - opp0;
+        int k = COLB(c.bcnt, jj);
+        if (k == 0) { COLB(c.border, norder) = (uint8_t)jj; norder++; }
+        size_t slot = (size_t)(jj * S.nmax + k) * E + env;
+        S.bear_val[slot] = bearing;
+        S.bear_ship[slot] = (uint8_t)i;
+        COLB(c.bcnt, jj) = (uint8_t)(k + 1);
+      }
+    }
+  }
+
+  // target list: observed positions first (combatant.py:152-154)
+  const int T = P.T;
+  uint16_t *tl = S.tl + (size_t)me * T * E + env;
+  int tn = 0;
+  for (int q = 0; q < obs_n; q++) {
+    uint32_t pk = COLW(c.observed, q);
+    tl[(size_t)tn * E] = (uint16_t)(pos_x(pk) | (pos_y(pk) << 8));
+    tn++;
+  }
+  // EW fixes (combatant.py:128-150) and fix targets (combatant.py:156-161)
+  for (int o = 0; o < norder; o++) {
+    int jj = COLB(c.border, o);
+    int n = COLB(c.bcnt, jj);
+    if (n < 2) continue;
+    bool zero = false;
+    auto slot = [&](int k) { return (size_t)(jj * S.nmax + k) * E + env; };
+    // consecutive-pair fixes summed in np.mean's order (pairwise for >= 8)
+    double sumx = 0.0, sumy = 0.0;
+    int m = n - 1;
+    double r0x = 0, r1x = 0, r2x = 0, r3x = 0, r4x = 0, r5x = 0, r6x = 0, r7x = 0;
+    double r0y = 0, r1y = 0, r2y = 0, r3y = 0, r4y = 0, r5y = 0, r6y = 0, r7y = 0;
+    int mblk = m - (m % 8);
+    bool tail_started = false;
+    double resx = 0.0, resy = 0.0;
+    for (int k = 0; k < m; k++) {
+      uint8_t s1 = S.bear_ship[slot(k)], s2 = S.bear_ship[slot(k + 1)];
+      double b1 = S.bear_val[slot(k)], b2 = S.bear_val[slot(k + 1)];
+      uint32_t p1 = COLW(c.pos_cur, s1), p2 = COLW(c.pos_cur, s2);
+      double x1 = pos_x(p1), y1 = pos_y(p1), x2 = pos_x(p2), y2 = pos_y(p2);
+      // calculate_fixed_position (combatant.py:265-277)
+      double m1 = tan(b1 * DEG2RAD);
+      double m2 = tan(b2 * DEG2RAD);
+      if (m1 - m2 == 0.0) { zero = true; break; }
+      double x3 = (m1 * x1 - m2 * x2 + y2 - y1) / (m1 - m2);
+      double y3 = m1 * (x3 - x1) + y1;
+      if (m < 8) {
+        sumx += x3;
+        sumy += y3;
+      } else if (k < 8) {
+        switch (k) {
+          case 0: r0x = x3; r0y = y3; break;
+          case 1: r1x = x3; r1y = y3; break;
+          case 2: r2x = x3; r2y = y3; break;
+          case 3: r3x = x3; r3y = y3; break;
+          case 4: r4x = x3; r4y = y3; break;
+          case 5: r5x = x3; r5y = y3; break;
+          case 6: r6x = x3; r6y = y3; break;
+          default: r7x = x3; r7y = y3; break;
+        }
+      } else if (k < mblk) {
+        switch (k & 7) {
+          case 0: r0x += x3; r0y += y3; break;
+          case 1: r1x += x3; r1y += y3; break;
+          case 2: r2x += x3; r2y += y3; break;
+          case 3: r3x += x3; r3y += y3; break;
+          case 4: r4x += x3; r4y += y3; break;
+          case 5: r5x += x3; r5y += y3; break;
+          case 6: r6x += x3; r6y += y3; break;
+          default: r7x += x3; r7y += y3; break;
+        }
+      } else {
+        if (!tail_started) {
+          resx = ((r0x + r1x) + (r2x + r3x)) + ((r4x + r5x) + (r6x + r7x));
+          resy = ((r0y + r1y) + (r2y + r3y)) + ((r4y + r5y) + (r6y + r7y));
+          tail_started = true;
+        }
+        resx += x3;
+        resy += y3;
+      }
+    }
+    if (zero) { X.rng.err |= LNW_ERRF_ZERODIV; continue; }
+    double mx, my;
+    if (m < 8) {
+      mx = sumx / (double)m;
+      my = sumy / (double)m;
+    } else {
+      if (!tail_started) {
+        resx = ((r0x + r1x) + (r2x + r3x)) + ((r4x + r5x) + (r6x + r7x));
+        resy = ((r0y + r1y) + (r2y + r3y)) + ((r4y + r5y) + (r6y + r7y));
+      }
+      mx = resx / (double)m;
+      my = resy / (double)m;
+    }
+    if (!isfinite(mx) || !isfinite(my)) { X.rng.err |= LNW_ERRF_NAN_ROUND; continue; }
+    double rx = rint(mx), ry = rint(my);
+    if (!(rx >= 0.0 && rx < (double)P.G && ry >= 0.0 && ry < (double)P.G)) continue;
+    int fxi = (int)rx, fyi = (int)ry;
+    for (int j = opp0; j < opp1; j++) {
+      if (!COLB(c.alive0, j)) continue;
+      uint32_t pj = COLW(c.pos_cur, j);
+      int ddx = pos_x(pj) - fxi, ddy = pos_y(pj) - fyi;
+      if (ddx * ddx + ddy * ddy < 4) {
+        tl[(size_t)tn * E] = (uint16_t)(fxi | (fyi << 8));
+        tn++;
+      }
+    }
+  }
+  COLW(c.tcnt, me) = (uint32_t)tn;
+}
+
+// check_target (combatant.py:570-584): first live opponent within 3.5 cells
+__device__ inline int check_target_dev(Ctx &X, int side, int tx, int ty) {
+  const KParams &P = X.P;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  int opp0 = side ? 0 : P.nb, opp1 = side ? P.nb : P.A;
+  for (int j = opp0; j < opp1; j++) {
+    if (!COLB(c.alive0, j)) continue;
+    uint32_t pj = COLW(c.pos_cur, j);
+    int dx = pos_x(pj) - tx, dy = pos_y(pj) - ty;
+    if (dx * dx + dy * dy <= 12) return j;
+  }
+  return -1;
+}
+
+struct Neut {
+  int cnt[2];
+  uint32_t mask[2];
+};
+
+// fire_missile (combatant.py:587-668) — returns hit
+__device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int ksalvo, Neut &N) {
+  const KParams &P = X.P;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const int side = a >= P.nb;
+  int t = check_target_dev(X, side, tx, ty);
+  if (t < 0) return false;
+  uint32_t pt = COLW(c.pos_cur, t), pa = COLW(c.pos_cur, a);
+  int dx = pos_x(pt) - pos_x(pa), dy = pos_y(pt) - pos_y(pa);
+  bool hit = false;
+  if (dx * dx + dy * dy < 4) {
+    hit = true;  // main gun, no draw
+  } else {
+    int miss = COLB(c.miss_cur, a);
+    if (miss == 0) return false;
+    int mk = COLB(c.mkind, a);
+    double u1 = X.rng.uniform();
+    bool detected = !(u1 < P.det_q[COLW(c.radar_cur, t) == 1 ? 0 : 1]);
+    int hp = detected ? 0 : 1;
+    double num;
+    int kn;
+    if (!P.discrete) {
+      int kp = kind_promote(mk, ksalvo);
+      if (kp == K_F32) {
+        num = (double)rintf((float)miss * (float)salvo);
+        kn = K_F32;
+      } else {
+        num = rint((double)miss * salvo);
+        kn = K_F64;  // np.round -> np.float64
+      }
+    } else {
+      num = COLB(c.type, a) == T_SMALL ? salvo : salvo * 2.0;
+      kn = K_PYINT;
+    }
+    if (num > (double)miss) { num = (double)miss; kn = mk; }
+    int n = (int)num;
+    COLB(c.miss_cur, a) = (uint8_t)(miss - n);
+    COLB(c.mkind, a) = (uint8_t)kind_promote(mk, kn);
+    double u2 = X.rng.uniform();
+    if (n < 0 || n > 8) { X.rng.err |= LNW_ERRF_MISSILES; n = n < 0 ? 0 : 8; }
+    if (kn == K_F32)
+      hit = (float)u2 < P.hit32[hp][n];
+    else
+      hit = u2 < P.hit64[hp][n];
+  }
+  if (hit) {
+    int ts = t >= P.nb;
+    N.cnt[ts]++;
+    N.mask[ts] |= 1u << (t - (ts ? P.nb : 0));
+  }
+  return hit;
+}
+
+// calculate_reward (game.py:214-295)
+__device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int n_hit) {
+  const KParams &P = X.P;
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  size_t ai = (size_t)a * X.E + X.env;
+  int steps = S.steps[ai] + 1;
+  S.steps[ai] = steps;
+  int tl_n = (int)COLW(c.tcnt, a);
+  double r = 0.0;
+  if (tl_n > 0) r += (double)(tl_n * 3);
+  if (moved) r += 1.0;
+  else r = fmax(r - 0.5, 0.0);
+  if (tl_n > 0 && !engage) r = r / 2.0;
+  else if (tl_n > 0 && engage && n_hit == 0) r += 0.5;
+  r += (double)(n_hit * 10);
+  int t = COLB(c.type, a);
+  uint32_t p = COLW(c.pos_cur, a);
+  int x = pos_x(p), y = pos_y(p);
+  bool red = a >= P.nb;
+  if (red && t != T_LS && !P.aggressive) {
+    if (steps > 14) {
+      if (x < 19 || x > 55 || y < 40 || y > 70) r = fmax(r - 2.0, 0.0);
+      else r += 1.0;
+    }
+  }
+  if (red && P.aggressive && t != T_LS) {
+    int dx = x - 15, dy = y - 60;
+    double nom = fmax(sqrt((double)(dx * dx + dy * dy)), 1.0);
+    double d = (1.0 / (nom / P.den[mast_cls(t)])) * 1.0;
+    r += d;
+  }
+  if (t == T_LS) {
+    int dx = x - P.lz_x, dy = y - P.lz_y;
+    double dl = sqrt((double)(dx * dx + dy * dy));
+    if (dl > 0) {
+      double cur = S.dist_lz[ai];
+      if (dl < cur) { r += 1.0; S.dist_lz[ai] = dl; }
+      else r -= 1.0;
+    } else {
+      r += 100.0;
+    }
+    if (dl == 0) r += 100.0;
+    else r += log10(100.0 / dl) * 5.0;
+  }
+  return r;
+}
+
+// Game.reset for one env (game.py:528-613), in-kernel
+__device__ void reset_env_dev(const KParams &P, const KState &S, int env, Rng &rng) {
+  const long long E = P.E;
+  double duct = 1.0 + rng.beta13();
+  S.duct[env] = duct;
+  // optional "box" spawn stream (build-side melee scenario)
+  bool box = P.box_hi[0] > P.box_lo[0] && P.box_hi[1] > P.box_lo[1];
+  unsigned long long box_ctr = ((unsigned long long)(uint32_t)S.envi[7 * E + env]) << 32;
+  for (int a = 0; a < P.A; a++) {
+    size_t ai = (size_t)a * E + env;
+    int t = S.sp_types[a];
+    int x, y;
+    if (S.sp_pos_env) {
+      x = S.sp_pos_env[((size_t)env * P.A + a) * 2];
+      y = S.sp_pos_env[((size_t)env * P.A + a) * 2 + 1];
+    } else {
+      x = S.sp_pos[2 * a];
+      y = S.sp_pos[2 * a + 1];
+    }
+    if (box) {
+      for (int tries = 0; tries < 64; tries++) {
+        uint32_t o[4];
+        o[0] = (uint32_t)box_ctr;
+        o[1] = (uint32_t)(box_ctr >> 32);
+        o[2] = rng.g0;
+        o[3] = rng.g1 ^ 0x80000000u;
+        philox10(o, rng.k0 ^ 0x5bd1e995u, rng.k1);
+        box_ctr++;
+        int bx = P.box_lo[0] + (int)(o[0] % (uint32_t)(P.box_hi[0] - P.box_lo[0]));
+        int by = P.box_lo[1] + (int)(o[1] % (uint32_t)(P.box_hi[1] - P.box_lo[1]));
+        if (!(cell_bits(S.mask2, P.W16, bx, by) & 1u)) { x = bx; y = by; break; }
+      }
+    }
+    if (S.sp_randls[a]) {
+      x = rng.randint(98, 99);
+      y = rng.randint(48, 56);
+    }
+    S.pos[ai] = pack_pos(x, y);
+    S.radar[ai] = 1;
+    S.miss[ai] = (uint8_t)missiles0(t);
+    S.mkind[ai] = K_PYINT;
+    S.alive[ai] = 1;
+    S.type[ai] = (uint8_t)t;
+    S.steps[ai] = 0;
+    S.tl_cnt[ai] = 0;
+    double dl = 0.0;
+    if (t == T_LS) {
+      int dx = x - P.lz_x, dy = y - P.lz_y;
+      dl = sqrt((double)(dx * dx + dy * dy));
+    }
+    S.dist_lz[ai] = dl;
+  }
+  S.envi[0 * E + env] = P.nb;
+  S.envi[1 * E + env] = P.nr;
+  S.envi[2 * E + env] = 0;
+  S.envi[3 * E + env] = 0;
+  S.envi[4 * E + env] = 0;
+  S.envi[7 * E + env] = S.envi[7 * E + env] + 1;
+}
+
+__device__ inline Rng make_rng(const KParams &P, const KState &S, int env) {
+  Rng r;
+  r.mode = P.rng_mode;
+  r.k0 = (uint32_t)P.seed;
+  r.k1 = (uint32_t)(P.seed >> 32);
+  unsigned long long gid = (unsigned long long)(P.env_base + env);
+  r.g0 = (uint32_t)gid;
+  r.g1 = (uint32_t)(gid >> 32);
+  r.ctr = S.rng[env];
+  r.err = 0;
+  r.tape = S.tape;
+  if (P.rng_mode == 1 && S.tape_off) {
+    r.tape_lo = S.tape_off[env];
+    r.tape_hi = S.tape_off[env + 1];
+  } else {
+    r.tape_lo = r.tape_hi = 0;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// phase O: observation vectors (combatant.py:163-233, landingship.py:167-239)
+// ---------------------------------------------------------------------------
+__device__ void write_obs(const KParams &P, const KState &S, Cols &c, const double *duct_col,
+                          int side, float *out, int env0, int nenv, bool only_observed) {
+  const int lane = threadIdx.x;
+  const int ns = side ? P.nr : P.nb;
+  const int own0 = side ? P.nb : 0;
+  const int D = 4 * ns + 52;
+  const int Bs = ns * D;
+  const int G = P.G;
+  for (int base = 0; base < Bs; base += WAVE) {
+    const int r = base + lane;
+    const bool valid = r < Bs;
+    const int kl = valid ? r / D : 0;
+    const int d = valid ? r - kl * D : 0;
+    const int k = own0 + kl;
+    for (int el = 0; el < nenv; el++) {
+      float v = 0.0f;
+      if (valid && c.alive0[k * PADB + el] && (!only_observed || c.obsd[k * PADB + el])) {
+        const int tk = c.type[k * PADB + el];
+        const int Wn = tk == T_LS ? 25 : 49;
+        if (d < Wn) {
+          uint32_t p = c.pos_cur[k * PAD + el];
+          int x, y;
+          if (tk == T_LS) { x = pos_x(p) - 1 + d / 5; y = pos_y(p) - 1 + d % 5; }
+          else { x = pos_x(p) - 3 + d / 7; y = pos_y(p) - 3 + d % 7; }
+          if (0 <= x && x < 100 && 0 <= y && y < 100)
+            v = (float)((double)S.grid[x * G + y] / 255.0);
+        } else {
+          const int t = d - Wn;
+          if (t < 4) {
+            uint32_t p = c.pos_cur[k * PAD + el];
+            if (t == 0) v = (float)((double)pos_x(p) / (double)G);
+            else if (t == 1) v = (float)((double)pos_y(p) / (double)G);
+            else if (t == 2) v = (float)c.radar_cur[k * PAD + el];
+            else v = (float)((double)c.miss_cur[k * PADB + el] / miss_norm(tk));
+          } else if (t < 4 * ns) {
+            int j = (t - 4) >> 2, f = (t - 4) & 3;
+            int il = j < kl ? j : j + 1;
+            int i = own0 + il;
+            if (c.alive0[i * PADB + el]) {
+              bool nw = il <= kl;
+              int ti = c.type[i * PADB + el];
+              if (f < 2) {
+                uint32_t p = nw ? c.pos_cur[i * PAD + el] : c.pos_old[i * PAD + el];
+                v = (float)((double)(f == 0 ? pos_x(p) : pos_y(p)) / (double)G);
+              } else if (f == 2) {
+                v = (float)(nw ? c.radar_cur[i * PAD + el] : c.radar_old[i * PAD + el]);
+              } else {
+                int m = nw ? c.miss_cur[i * PADB + el] : c.miss_old[i * PADB + el];
+                v = (float)((double)m / miss_norm(ti));
+              }
+            }
+          } else if (t == 4 * ns) {
+            v = (float)c.tcnt[k * PAD + el];
+          } else if (t == 4 * ns + 1) {
+            v = tk == T_LS ? 1.0f : 0.0f;
+          } else if (t == 4 * ns + 2) {
+            v = (float)(duct_col[el] / 2.0);
+          }
+        }
+      }
+      if (valid) out[(size_t)(env0 + el) * Bs + r] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// phase L: load state columns
+// ---------------------------------------------------------------------------
+__device__ inline void load_state(const KParams &P, const KState &S, Cols &c, int lane, int env,
+                                  bool valid) {
+  const long long E = P.E;
+  for (int a = 0; a < P.A; a++) {
+    size_t ai = (size_t)a * E + env;
+    if (valid) {
+      uint32_t p = S.pos[ai];
+      COLW(c.pos_cur, a) = p;
+      COLW(c.pos_old, a) = p;
+      COLW(c.pos_new, a) = p;
+      int rd = S.radar[ai];
+      COLW(c.radar_cur, a) = rd;
+      COLW(c.radar_old, a) = rd;
+      uint8_t m = S.miss[ai];
+      COLB(c.miss_cur, a) = m;
+      COLB(c.miss_old, a) = m;
+      COLB(c.mkind, a) = S.mkind[ai];
+      COLB(c.type, a) = S.type[ai];
+      COLB(c.alive0, a) = S.alive[ai];
+      COLW(c.tcnt, a) = S.tl_cnt[ai];
+      COLB(c.eng, a) = 0;
+      COLB(c.obsd, a) = 0;
+    } else {
+      COLB(c.alive0, a) = 0;
+      COLB(c.type, a) = 0;
+    }
+  }
+}
+
+extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+
+// ---------------------------------------------------------------------------
+// step kernel (Game.step, game.py:298-525)
+// ---------------------------------------------------------------------------
+template <bool MARCH>
+__global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *actions,
+                                                  const uint8_t *row_kind, float *obs_b,
+                                                  float *obs_r, float *rew_b, float *rew_r,
+                                                  int32_t *done_out, float *cog_out) {
+  const int lane = threadIdx.x;
+  const int env0 = blockIdx.x * WAVE;
+  const int env = env0 + lane;
+  const long long E = P.E;
+  const bool valid = env < E;
+  const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
+  const int A = P.A, nb = P.nb, nr = P.nr;
+  LdsLayout L = lds_layout(A, S.nmax, MARCH ? P.G * P.W16 : 0);
+  Cols c = carve(lds_dyn, L);
+  __shared__ double duct_col[WAVE];
+
+  const uint32_t *mask = S.mask2;
+  if (MARCH) {
+    for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
+    mask = c.mask;
+  }
+  load_state(P, S, c, lane, env, valid);
+  double duct = valid ? S.duct[env] : 1.0;
+  duct_col[lane] = duct;
+  __syncthreads();
+
+  // ---- phase M: movement feasibility for every agent of this env --------
+  const int dt = P.act_dtype;
+  if (valid) {
+    for (int a = 0; a < A; a++) {
+      if (!COLB(c.alive0, a)) continue;
+      uint32_t p = COLW(c.pos_old, a);
+      int sx = pos_x(p), sy = pos_y(p);
+      int t = COLB(c.type, a);
+      size_t row = ((size_t)env * A + a) * 4;
+      bool feas = false;
+      int tx = sx, ty = sy;
+      if (dt == LNW_ACT_I32) {
+        int v = ((const int32_t *)actions)[row + 2];
+        int x = floordiv7(v), y = pymod7(v);
+        if (0 <= sx - 3 + x && sx - 3 + x < P.G && 0 <= sy - 3 + y && sy - 3 + y < P.G) {
+          tx = sx - 3 + x;
+          ty = sy - 3 + y;
+          feas = check_path_h(P, S, t, sx, sy, tx, ty, c.open + lane, WAVE);
+        }
+      } else {
+        double a2, a3;
+        int kind;
+        if (dt == LNW_ACT_F32) {
+          const float *fa = (const float *)actions;
+          a2 = fa[row + 2];
+          a3 = fa[row + 3];
+          kind = K_F32;
+        } else {
+          const double *da = (const double *)actions;
+          a2 = da[row + 2];
+          a3 = da[row + 3];
+          kind = row_kind ? row_kind[(size_t)env * A + a] : K_F64;
+        }
+        int nx, ny;
+        bool ok = move_target_dev(sx, sy, ship_speed(t), a2, a3, kind, nx, ny);
+        if (!ok) {
+          S.err[env] |= LNW_ERRF_NAN_ROUND;
+        } else if (can_move_to_h(P, S, nx, ny)) {
+          feas = check_path_h(P, S, t, sx, sy, nx, ny, c.open + lane, WAVE);
+          tx = nx;
+          ty = ny;
+        }
+      }
+      COLW(c.pos_new, a) = feas ? (pack_pos(tx, ty) | 0x80000000u) : p;
+    }
+  }
+
+  // ---- phase S: sequential agent loop ------------------------------------
+  int done = 1;
+  float cog = NAN;
+  if (valid) {
+    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E};
+    Neut N{{0, 0}, {0u, 0u}};
+    int hits[2] = {0, 0};
+    double bsx = 0, bsy = 0, rsx = 0, rsy = 0;
+    int nbp = 0, nrp = 0;
+    for (int a = 0; a < A; a++) {
+      if (!COLB(c.alive0, a)) { COLW(c.reward, a) = 0.0; continue; }
+      const int side = a >= nb;
+      uint32_t p0 = COLW(c.pos_cur, a);
+      if (!side) {
+        if (P.side_blue) { bsx += pos_x(p0); bsy += pos_y(p0); nbp++; }
+      } else {
+        rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
+      }
+      size_t row = ((size_t)env * A + a) * 4;
+      double a0, a1;
+      int kind;
+      if (dt == LNW_ACT_F32) {
+        const float *fa = (const float *)actions;
+        a0 = fa[row]; a1 = fa[row + 1]; kind = K_F32;
+      } else if (dt == LNW_ACT_F64) {
+        const double *da = (const double *)actions;
+        a0 = da[row]; a1 = da[row + 1];
+        kind = row_kind ? row_kind[(size_t)env * A + a] : K_F64;
+      } else {
+        const int32_t *ia = (const int32_t *)actions;
+        a0 = ia[row]; a1 = ia[row + 1]; kind = K_PYINT;
+      }
+      // untrained red: random salvo (game.py:375-379), written back in place
+      if (side && !P.trained_red) {
+        if (X.rng.uniform() < P.red_aggression) {
+          double v = X.rng.uniform();
+          if (dt == LNW_ACT_F32) { float f = (float)v; ((float *)actions)[row + 1] = f; a1 = f; }
+          else if (dt == LNW_ACT_F64) {
+            if (kind == K_F32) v = (double)(float)v;
+            ((double *)actions)[row + 1] = v; a1 = v;
+          } else { ((int32_t *)actions)[row + 1] = 0; a1 = 0.0; }
+        }
+      }
+      // take_action (combatant.py:501-565)
+      double engagement = P.discrete ? rint(a1) : a1;
+      int keng = P.discrete ? K_PYINT : kind;
+      int mk = COLB(c.mkind, a);
+      double thr_v;
+      if (kind_promote(keng, mk) == K_F32)
+        thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
+      else
+        thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
+      bool engage = thr_v > 0.0;
+      int destroyed = 0;
+      int tn = (int)COLW(c.tcnt, a);
+      if (engage && tn > 0) {
+        const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
+        for (int q = 0; q < tn; q++) {
+          uint16_t tg = tl[(size_t)q * E];
+          if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+        }
+      }
+      S.envi[(5 + side) * E + env] += destroyed;
+      if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
+      else {
+        double rr = rint(a0);
+        COLW(c.radar_cur, a) = (int)fmin(fmax(rr, -2147483648.0), 2147483647.0);
+      }
+      uint32_t pn = COLW(c.pos_new, a);
+      bool moved = (pn & 0x80000000u) != 0;
+      if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
+      get_obs_dev(X, a);
+      double r = reward_dev(X, a, moved, engage, destroyed);
+      COLW(c.reward, a) = r;
+      if (!side) {
+        if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
+      } else {
+        if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
+      }
+      hits[side] += destroyed;
+    }
+    // ---- tail (game.py:409-520) -------------------------------------------
+    int nbl = S.envi[0 * E + env] - N.cnt[0];
+    int nrl = S.envi[1 * E + env] - N.cnt[1];
+    S.envi[0 * E + env] = nbl;
+    S.envi[1 * E + env] = nrl;
+    bool no_blue = nbl == 0, no_red = nrl == 0;
+    for (int a = 0; a < A; a++) {
+      if (!COLB(c.alive0, a)) continue;
+      int side = a >= nb;
+      if (!COLB(c.eng, a)) COLW(c.reward, a) += (double)(hits[side] * 2);
+    }
+    if (!P.aggressive) {
+      for (int a = 0; a < A; a++) {
+        int side = a >= nb;
+        if (N.cnt[side] > 0) COLW(c.reward, a) = fmax(COLW(c.reward, a) - (double)(N.cnt[side] * 5), 0.0);
+      }
+    }
+    if (no_blue && !no_red) {
+      done = 0;
+      for (int a = 0; a < A; a++) {
+        if (a < nb) { if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a); }
+        else COLW(c.reward, a) += 100.0;
+      }
+      S.envi[4 * E + env] += 1;
+    }
+    if (no_red && !no_blue) {
+      done = 0;
+      for (int a = 0; a < A; a++) {
+        if (a < nb) COLW(c.reward, a) += 100.0;
+        else if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
+      }
+      S.envi[3 * E + env] += 1;
+    }
+    if (no_blue && no_red) {
+      done = 0;
+      for (int a = 0; a < A; a++) COLW(c.reward, a) += 10.0;
+    }
+    if (P.landing_ops) {
+      int rem = 0;
+      for (int a = nb; a < A; a++) rem += (COLB(c.alive0, a) && COLB(c.type, a) == T_LS) ? 1 : 0;
+      if (!rem) {
+        done = 0;
+        for (int a = 0; a < A; a++) {
+          if (a < nb) COLW(c.reward, a) += 100.0;
+          else COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
+        }
+        S.envi[3 * E + env] += 1;
+      } else {
+        for (int l = nb; l < A; l++) {
+          if (!(COLB(c.alive0, l) && COLB(c.type, l) == T_LS)) continue;
+          uint32_t pl = COLW(c.pos_cur, l);
+          if (pos_x(pl) == P.lz_x && pos_y(pl) == P.lz_y) {
+            done = 0;
+            for (int a = 0; a < A; a++) {
+              if (a < nb) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
+              else COLW(c.reward, a) += 100.0;
+            }
+            S.envi[3 * E + env] += 1;
+          }
+        }
+      }
+    }
+    int steps_env = S.envi[2 * E + env] + 1;
+    S.envi[2 * E + env] = steps_env;
+    if (nbp > 0 && nrp > 0) {
+      double bx = bsx / nbp, by = bsy / nbp, rx = rsx / nrp, ry = rsy / nrp;
+      cog = (float)sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
+    }
+    // outputs
+    for (int a = 0; a < nb; a++)
+      if (rew_b) rew_b[(size_t)env * nb + a] = (float)COLW(c.reward, a);
+    for (int a = 0; a < nr; a++)
+      if (rew_r) rew_r[(size_t)env * nr + a] = (float)COLW(c.reward, nb + a);
+    if (done_out) done_out[env] = done;
+    if (cog_out) cog_out[env] = cog;
+    // ---- phase W: store state (alive updated by the neutralized lists) --
+    bool do_reset = P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
+    for (int a = 0; a < A; a++) {
+      size_t ai = (size_t)a * E + env;
+      int side = a >= nb;
+      bool killed = (N.mask[side] >> (a - (side ? nb : 0))) & 1u;
+      S.pos[ai] = COLW(c.pos_cur, a);
+      S.radar[ai] = COLW(c.radar_cur, a);
+      S.miss[ai] = COLB(c.miss_cur, a);
+      S.mkind[ai] = COLB(c.mkind, a);
+      S.alive[ai] = COLB(c.alive0, a) && !killed;
+      S.tl_cnt[ai] = (uint16_t)COLW(c.tcnt, a);
+    }
+    if (do_reset) reset_env_dev(P, S, env, X.rng);
+    S.rng[env] = X.rng.ctr;
+    if (X.rng.err) S.err[env] |= X.rng.err;
+  }
+  __syncthreads();
+  // ---- phase O: observations ---------------------------------------------
+  if (obs_b) write_obs(P, S, c, duct_col, 0, obs_b, env0, nenv, false);
+  if (obs_r) write_obs(P, S, c, duct_col, 1, obs_r, env0, nenv, false);
+}
+
+// ---------------------------------------------------------------------------
+// observe kernel (ship.get_obs() for a selection of ships)
+// ---------------------------------------------------------------------------
+template <bool MARCH>
+__global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
+                                                     float *obs_r) {
+  const int lane = threadIdx.x;
+  const int env0 = blockIdx.x * WAVE;
+  const int env = env0 + lane;
+  const long long E = P.E;
+  const bool valid = env < E;
+  const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
+  const int A = P.A, nb = P.nb;
+  LdsLayout L = lds_layout(A, S.nmax, MARCH ? P.G * P.W16 : 0);
+  Cols c = carve(lds_dyn, L);
+  __shared__ double duct_col[WAVE];
+  const uint32_t *mask = S.mask2;
+  if (MARCH) {
+    for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
+    mask = c.mask;
+  }
+  load_state(P, S, c, lane, env, valid);
+  double duct = valid ? S.duct[env] : 1.0;
+  duct_col[lane] = duct;
+  __syncthreads();
+  if (valid) {
+    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E};
+    int a0 = 0, a1 = A;
+    if (sel >= 0) { a0 = sel; a1 = sel + 1; }
+    else if (sel == LNW_OBS_BLUE) { a1 = nb; }
+    else if (sel == LNW_OBS_RED) { a0 = nb; }
+    for (int a = a0; a < a1; a++) {
+      if (!COLB(c.alive0, a)) continue;
+      get_obs_dev(X, a);
+      COLB(c.obsd, a) = 1;
+      S.tl_cnt[(size_t)a * E + env] = (uint16_t)COLW(c.tcnt, a);
+    }
+    S.rng[env] = X.rng.ctr;
+    if (X.rng.err) S.err[env] |= X.rng.err;
+  }
+  __syncthreads();
+  // rows of ships not observed in this call are written as zeros
+  if (obs_b) write_obs(P, S, c, duct_col, 0, obs_b, env0, nenv, true);
+  if (obs_r) write_obs(P, S, c, duct_col, 1, obs_r, env0, nenv, true);
+}
+
+__global__ void reset_kernel(KParams P, KState S, const uint8_t *mask) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= P.E) return;
+  if (mask && !mask[env]) return;
+  Rng r = make_rng(P, S, env);
+  reset_env_dev(P, S, env, r);
+  S.rng[env] = r.ctr;
+  if (r.err) S.err[env] |= r.err;
+}
+
+// ---------------------------------------------------------------------------
+// terrain structures
+// ---------------------------------------------------------------------------
+__global__ void build_mask_kernel(const uint8_t *grid, int G, int W16, int move_thr, int ew_thr,
+                                  uint32_t *mask2) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= G * W16) return;
+  int x = i / W16, w = i % W16;
+  uint32_t v = 0;
+  for (int b = 0; b < 16; b++) {
+    int y = w * 16 + b;
+    if (y >= G) break;
+    uint8_t g = grid[x * G + y];
+    v |= ((g > move_thr ? 1u : 0u) | (g > ew_thr ? 2u : 0u)) << (2 * b);
+  }
+  mask2[i] = v;
+}
+
+// move table: check_path(start, start + off) for off in [-4,4]^2, per class
+__global__ __launch_bounds__(64) void build_move_table_kernel(const uint32_t *mask2, int G, int W16,
+                                                              uint32_t *mvtab) {
+  __shared__ uint32_t open[OPEN_CAP * WAVE];
+  long long i = (long long)blockIdx.x * WAVE + threadIdx.x;
+  long long n = 2LL * G * G * MV_W * MV_W;
+  if (i >= n) return;
+  int off = (int)(i % (MV_W * MV_W));
+  long long cell = (i / (MV_W * MV_W)) % ((long long)G * G);
+  int cls = (int)(i / ((long long)MV_W * MV_W * G * G));
+  int sx = (int)(cell / G), sy = (int)(cell % G);
+  int tx = sx + off / MV_W - R_MV, ty = sy + off % MV_W - R_MV;
+  MaskBlocked mb{mask2, W16};
+  bool feas = check_path_dev(mb, mb(sx, sy), G, cls ? T_LS : T_SMALL, sx, sy, tx, ty,
+                             open + threadIdx.x, WAVE);
+  if (feas) atomicOr(&mvtab[(cls * (long long)G * G + cell) * MV_WORDS + (off >> 5)], 1u << (off & 31));
+}
+
+// LOS table: for every origin cell and offset in [-40,40]^2, bit0 radar clear,
+// bit1 EW clear (full march, no early exit)
+__global__ void build_los_table_kernel(const uint32_t *mask2, int G, int W16, uint32_t *lostab) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long n = (long long)G * G * LOS_W;
+  if (i >= n) return;
+  int row = (int)(i % LOS_W);
+  long long cell = i / LOS_W;
+  int x1 = (int)(cell / G), y1 = (int)(cell % G);
+  int x2 = x1 + row - R_LOS;
+  uint32_t words[LOS_ROW_WORDS] = {0, 0, 0, 0, 0, 0};
+  if (x2 >= 0 && x2 < G) {
+    for (int c = 0; c < LOS_W; c++) {
+      int y2 = y1 + c - R_LOS;
+      if (y2 < 0 || y2 >= G) continue;
+      uint32_t b = los_march<false>(mask2, W16, x1, y1, x2, y2);
+      int col = c * 2;
+      words[col >> 5] |= b << (col & 31);
+    }
+  }
+  uint32_t *dst = lostab + cell * LOS_CELL_WORDS + row * LOS_ROW_WORDS;
+#pragma unroll
+  for (int w = 0; w < LOS_ROW_WORDS; w++) dst[w] = words[w];
+}
+
+// ---------------------------------------------------------------------------
+// unit kernels
+// ---------------------------------------------------------------------------
+__global__ void los_batch_kernel(const uint8_t *grid, int G, const int16_t *pairs, long long n,
+                                 int move_thr, int ew_thr, uint8_t *out) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int x1 = pairs[4 * i], y1 = pairs[4 * i + 1], x2 = pairs[4 * i + 2], y2 = pairs[4 * i + 3];
+  int dx = abs(x2 - x1), dy = abs(y2 - y1);
+  int sx = x1 > x2 ? -1 : 1, sy = y1 > y2 ? -1 : 1;
+  int err = dx - dy;
+  bool rb = false, eb = false;
+  for (;;) {
+    uint8_t g = grid[x1 * G + y1];
+    rb |= g > move_thr;
+    eb |= g > ew_thr;
+    if (x1 == x2 && y1 == y2) break;
+    int e2 = 2 * err;
+    if (e2 > -dy) { err -= dy; x1 += sx; }
+    if (e2 < dx) { err += dx; y1 += sy; }
+  }
+  out[i] = (rb ? 0 : 1) | (eb ? 0 : 2);
+}
+
+__global__ __launch_bounds__(64) void astar_batch_kernel(const uint8_t *grid, int G, int thr,
+                                                         const int8_t *types, const int16_t *st,
+                                                         const int16_t *tg, long long n,
+                                                         int16_t *plen, int8_t *kind,
+                                                         uint8_t *feas) {
+  __shared__ uint32_t open[OPEN_CAP * WAVE];
+  long long i = (long long)blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n) return;
+  int t = types[i];
+  int sx = st[2 * i], sy = st[2 * i + 1], tx = tg[2 * i], ty = tg[2 * i + 1];
+  GridBlocked gb{grid, G, thr};
+  if (abs(tx) > 500 || abs(ty) > 500 || sx < 0 || sy < 0 || sx >= G || sy >= G) {
+    plen[i] = -2; kind[i] = -1; feas[i] = 0;
+    return;
+  }
+  int k;
+  int len = astar_dev(gb, G, ship_speed(t), sx, sy, tx, ty, k, open + threadIdx.x, WAVE);
+  plen[i] = (int16_t)len;
+  kind[i] = (int8_t)k;
+  feas[i] = check_path_dev(gb, gb(sx, sy), G, t, sx, sy, tx, ty, open + threadIdx.x, WAVE) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void move_batch_kernel(KParams P, KState S, const int8_t *types,
+                                                        const int16_t *pos, const double *act,
+                                                        const uint8_t *is_f32, long long n,
+                                                        int32_t *rounded, uint8_t *ok) {
+  __shared__ uint32_t open[OPEN_CAP * WAVE];
+  long long i = (long long)blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n) return;
+  int t = types[i];
+  int sx = pos[2 * i], sy = pos[2 * i + 1];
+  int nx, ny;
+  bool fin = move_target_dev(sx, sy, ship_speed(t), act[2 * i], act[2 * i + 1],
+                             is_f32[i] ? K_F32 : K_F64, nx, ny);
+  rounded[2 * i] = nx;
+  rounded[2 * i + 1] = ny;
+  bool f = fin && can_move_to_h(P, S, nx, ny) &&
+           check_path_h(P, S, t, sx, sy, nx, ny, open + threadIdx.x, WAVE);
+  ok[i] = f ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void path_query_kernel(KParams P, KState S, const int8_t *types,
+                                                        const int16_t *st, const int16_t *tg,
+                                                        long long n, uint8_t *out) {
+  __shared__ uint32_t open[OPEN_CAP * WAVE];
+  long long i = (long long)blockIdx.x * WAVE + threadIdx.x;
+  if (i >= n) return;
+  out[i] = check_path_h(P, S, types[i], st[2 * i], st[2 * i + 1], tg[2 * i], tg[2 * i + 1],
+                        open + threadIdx.x, WAVE) ? 1 : 0;
+}
+
+__global__ void los_query_kernel(KParams P, KState S, const int16_t *pairs, long long n,
+                                 uint8_t *out) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = (uint8_t)los_q(P, S, S.mask2, pairs[4 * i], pairs[4 * i + 1], pairs[4 * i + 2],
+                          pairs[4 * i + 3]);
+}
+
+__global__ void fill_uniform_kernel(float *out, long long n, unsigned long long seed,
+                                    unsigned long long offset) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long base = i * 4;
+  if (base >= n) return;
+  unsigned long long ctr = (offset >> 2) + (unsigned long long)i;
+  uint32_t o[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x243F6A88u, 0x85A308D3u};
+  philox10(o, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (base + k < n) out[base + k] = (float)(o[k] >> 8) * 5.9604644775390625e-08f;
+}
+
+// ===========================================================================
+// host side
+// ===========================================================================
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(LNW_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));    \
+  } while (0)
+
+void host_constants(KParams &k) {
+  const double base = std::sqrt((4.0 / 3.0) * 6370.0 * 2.0);
+  const int masts[2] = {15, 30};
+  for (int i = 0; i < 2; i++)
+    for (int j = 0; j < 2; j++) {
+      double d = base * (std::sqrt((double)masts[i] / 1000.0) + std::sqrt((double)masts[j] / 1000.0));
+      k.d5[i][j] = d / 5.0;
+    }
+  for (int i = 0; i < 2; i++)
+    k.den[i] = (base * (std::sqrt((double)masts[i] / 1000.0) + std::sqrt(15.0 / 1000.0))) / 5.0;
+  k.det_q[0] = 0.345 - 0.1;
+  k.det_q[1] = 0.345 + 0.1;
+  const double ps[2] = {0.45, 0.63};
+  for (int h = 0; h < 2; h++)
+    for (int n = 0; n < 9; n++) {
+      k.hit64[h][n] = 1.0 - std::pow(1.0 - ps[h], (double)n);
+      float pn = powf((float)(1.0 - ps[h]), (float)n);
+      k.hit32[h][n] = 1.0f - pn;
+    }
+}
+
+}  // namespace
+
+struct lnw_handle {
+  int device = 0;
+  lnw_params params{};
+  KParams kp{};
+  int E = 0, nb = 0, nr = 0, A = 0, T = 0, nmax = 0;
+  long long env_base = 0;
+  int G = 0, W16 = 0;
+  bool terrain = false;
+  // device buffers
+  uint8_t *d_grid = nullptr;
+  uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
+  uint32_t *pos = nullptr;
+  int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
+  uint8_t *miss = nullptr, *mkind = nullptr, *alive = nullptr, *type = nullptr;
+  double *dist_lz = nullptr, *duct = nullptr, *bear_val = nullptr;
+  uint8_t *bear_ship = nullptr;
+  uint16_t *tl_cnt = nullptr, *tl = nullptr;
+  unsigned long long *rng = nullptr;
+  uint32_t *err = nullptr;
+  int32_t *sp_types = nullptr, *sp_pos = nullptr, *sp_randls = nullptr, *sp_pos_env = nullptr;
+  const double *tape = nullptr;
+  const long long *tape_off = nullptr;
+  std::vector<void *> allocs;
+};
+
+namespace {
+
+template <class T>
+int dalloc(lnw_handle *h, T **p, size_t n) {
+  void *q = nullptr;
+  hipError_t e = hipMalloc(&q, n * sizeof(T) + 16);
+  if (e != hipSuccess) return fail(LNW_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  (void)hipMemset(q, 0, n * sizeof(T) + 16);
+  h->allocs.push_back(q);
+  *p = (T *)q;
+  return 0;
+}
+
+KState make_state(lnw_handle *h) {
+  KState s{};
+  s.pos = h->pos; s.radar = h->radar; s.miss = h->miss; s.mkind = h->mkind; s.alive = h->alive;
+  s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
+  s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
+  s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
+  s.grid = h->d_grid; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.tape = h->tape; s.tape_off = h->tape_off;
+  s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
+  s.sp_pos_env = nullptr;
+  s.nmax = h->nmax;
+  return s;
+}
+
+size_t step_lds_bytes(const lnw_handle *h, bool march) {
+  LdsLayout L = lds_layout(h->A, h->nmax, march ? h->G * h->W16 : 0);
+  return (size_t)L.total;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lnw_abi_version(void) { return LNW_ABI_VERSION; }
+const char *lnw_last_error(void) { return g_err.c_str(); }
+
+int lnw_hit_tables(double *tab64, float *tab32) {
+  KParams k{};
+  host_constants(k);
+  for (int h = 0; h < 2; h++)
+    for (int n = 0; n < 9; n++) {
+      if (tab64) tab64[h * 9 + n] = k.hit64[h][n];
+      if (tab32) tab32[h * 9 + n] = k.hit32[h][n];
+    }
+  return 0;
+}
+
+int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr, int32_t device,
+               int64_t env_id_base, lnw_handle **out) {
+  if (!params || !out) return fail(LNW_EINVAL, "null argument");
+  if (n_envs <= 0) return fail(LNW_EINVAL, "n_envs must be > 0");
+  if (nb < 1 || nr < 1 || nb > 16 || nr > 16)
+    return fail(LNW_EUNSUPPORTED, "need 1 <= nb, nr <= 16 ships per side");
+  HIPCHK(hipSetDevice(device));
+  lnw_handle *h = new lnw_handle();
+  h->device = device;
+  h->params = *params;
+  h->E = n_envs; h->nb = nb; h->nr = nr; h->A = nb + nr;
+  h->nmax = nb > nr ? nb : nr;
+  h->T = h->nmax + h->nmax * h->nmax;
+  h->env_base = env_id_base;
+  const size_t E = (size_t)n_envs, A = (size_t)h->A;
+  int rc = 0;
+  rc |= dalloc(h, &h->pos, A * E);
+  rc |= dalloc(h, &h->radar, A * E);
+  rc |= dalloc(h, &h->miss, A * E);
+  rc |= dalloc(h, &h->mkind, A * E);
+  rc |= dalloc(h, &h->alive, A * E);
+  rc |= dalloc(h, &h->type, A * E);
+  rc |= dalloc(h, &h->steps, A * E);
+  rc |= dalloc(h, &h->dist_lz, A * E);
+  rc |= dalloc(h, &h->tl_cnt, A * E);
+  rc |= dalloc(h, &h->tl, A * (size_t)h->T * E);
+  rc |= dalloc(h, &h->duct, E);
+  rc |= dalloc(h, &h->envi, 8 * E);
+  rc |= dalloc(h, &h->rng, E);
+  rc |= dalloc(h, &h->err, E);
+  rc |= dalloc(h, &h->bear_val, (size_t)h->nmax * h->nmax * E);
+  rc |= dalloc(h, &h->bear_ship, (size_t)h->nmax * h->nmax * E);
+  rc |= dalloc(h, &h->sp_types, 64);
+  rc |= dalloc(h, &h->sp_pos, 128);
+  rc |= dalloc(h, &h->sp_randls, 64);
+  if (rc) {
+    std::string m = g_err;
+    lnw_destroy(h);
+    return fail(LNW_ENOMEM, m);
+  }
+  KParams &k = h->kp;
+  k.discrete = params->discrete; k.landing_ops = params->landing_ops;
+  k.aggressive = params->aggressive; k.side_blue = params->side_blue;
+  k.trained_red = params->trained_red; k.move_thr = params->move_thr; k.ew_thr = params->ew_thr;
+  k.lz_x = params->lz_x; k.lz_y = params->lz_y; k.red_aggression = params->red_aggression;
+  k.episode_steps = params->episode_steps; k.auto_reset = params->auto_reset;
+  k.los_mode = params->los_mode; k.move_mode = params->move_mode;
+  k.E = n_envs; k.nb = nb; k.nr = nr; k.A = h->A; k.T = h->T;
+  k.env_base = env_id_base;
+  k.rng_mode = LNW_RNG_PHILOX;
+  k.seed = 0;
+  host_constants(k);
+  *out = h;
+  return 0;
+}
+
+int lnw_destroy(lnw_handle *h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  for (void *p : h->allocs) (void)hipFree(p);
+  delete h;
+  return 0;
+}
+
+int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
+  if (!h || !grid_host) return fail(LNW_EINVAL, "null argument");
+  if (G < 8 || G > 1024) return fail(LNW_EINVAL, "grid size out of range");
+  HIPCHK(hipSetDevice(h->device));
+  h->G = G;
+  h->W16 = (G + 15) / 16;
+  int rc = 0;
+  if (h->d_grid) {  // re-load: release the previous terrain structures
+    HIPCHK(hipDeviceSynchronize());
+    void *old[4] = {h->d_grid, h->d_mask2, h->d_mvtab, h->d_lostab};
+    for (void *p : old) {
+      for (size_t i = 0; i < h->allocs.size(); i++)
+        if (h->allocs[i] == p) { (void)hipFree(p); h->allocs.erase(h->allocs.begin() + i); break; }
+    }
+  }
+  rc |= dalloc(h, &h->d_grid, (size_t)G * G);
+  rc |= dalloc(h, &h->d_mask2, (size_t)G * h->W16);
+  rc |= dalloc(h, &h->d_mvtab, (size_t)2 * G * G * MV_WORDS);
+  rc |= dalloc(h, &h->d_lostab, (size_t)G * G * LOS_CELL_WORDS);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(h->d_grid, grid_host, (size_t)G * G, hipMemcpyHostToDevice));
+  KParams &k = h->kp;
+  k.G = G;
+  k.W16 = h->W16;
+  int n = G * h->W16;
+  build_mask_kernel<<<(n + 255) / 256, 256>>>(h->d_grid, G, h->W16, k.move_thr, k.ew_thr, h->d_mask2);
+  HIPCHK(hipGetLastError());
+  long long nm = 2LL * G * G * MV_W * MV_W;
+  build_move_table_kernel<<<(unsigned)((nm + WAVE - 1) / WAVE), WAVE>>>(h->d_mask2, G, h->W16, h->d_mvtab);
+  HIPCHK(hipGetLastError());
+  long long nl = (long long)G * G * LOS_W;
+  build_los_table_kernel<<<(unsigned)((nl + 255) / 256), 256>>>(h->d_mask2, G, h->W16, h->d_lostab);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  h->terrain = true;
+  // large dynamic LDS for the march variants
+  (void)hipFuncSetAttribute((const void *)step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void *)step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void *)observe_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void *)observe_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  return 0;
+}
+
+int lnw_set_rng(lnw_handle *h, int32_t mode, uint64_t seed, const double *tape_dev,
+                const int64_t *tape_off_dev) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  if (mode != LNW_RNG_PHILOX && mode != LNW_RNG_TAPE) return fail(LNW_EINVAL, "bad rng mode");
+  if (mode == LNW_RNG_TAPE && (!tape_dev || !tape_off_dev))
+    return fail(LNW_EINVAL, "tape mode needs tape and offsets");
+  HIPCHK(hipSetDevice(h->device));
+  h->kp.rng_mode = mode;
+  h->kp.seed = seed;
+  h->tape = tape_dev;
+  h->tape_off = (const long long *)tape_off_dev;
+  HIPCHK(hipMemset(h->rng, 0, sizeof(unsigned long long) * h->E));
+  return 0;
+}
+
+int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn,
+              const int32_t *pos_dev, void *stream) {
+  if (!h || !spawn) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  HIPCHK(hipSetDevice(h->device));
+  for (int a = 0; a < h->A; a++) {
+    int t = spawn->types[a];
+    if (t != LNW_SMALL && t != LNW_LARGE && t != LNW_LS)
+      return fail(LNW_EUNSUPPORTED, "ship type must be small, large or ls");
+    if (h->params.discrete && t == LNW_LS)
+      return fail(LNW_EUNSUPPORTED, "LandingShip has no value_to_coordinates (DISCRETE mode)");
+    if (!spawn->rand_ls[a] && (spawn->pos[a][0] < 0 || spawn->pos[a][0] >= h->G ||
+                               spawn->pos[a][1] < 0 || spawn->pos[a][1] >= h->G))
+      return fail(LNW_EINVAL, "spawn position outside the grid");
+  }
+  hipStream_t st = (hipStream_t)stream;
+  HIPCHK(hipMemcpy(h->sp_types, spawn->types, sizeof(int32_t) * h->A, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->sp_pos, spawn->pos, sizeof(int32_t) * 2 * h->A, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->sp_randls, spawn->rand_ls, sizeof(int32_t) * h->A, hipMemcpyHostToDevice));
+  h->kp.box_lo[0] = spawn->box_lo[0]; h->kp.box_lo[1] = spawn->box_lo[1];
+  h->kp.box_hi[0] = spawn->box_hi[0]; h->kp.box_hi[1] = spawn->box_hi[1];
+  KState s = make_state(h);
+  s.sp_pos_env = pos_dev;
+  reset_kernel<<<(h->E + 255) / 256, 256, 0, st>>>(h->kp, s, env_mask_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
+             float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
+             int32_t *done_dev, float *cog_dev, void *stream) {
+  if (!h || !actions_dev) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  if (action_dtype != LNW_ACT_F32 && action_dtype != LNW_ACT_F64 && action_dtype != LNW_ACT_I32)
+    return fail(LNW_EINVAL, "bad action dtype");
+  if ((action_dtype == LNW_ACT_I32) != (h->params.discrete != 0))
+    return fail(LNW_EINVAL, "integer actions go with DISCRETE mode and only with it");
+  KParams k = h->kp;
+  k.act_dtype = action_dtype;
+  KState s = make_state(h);
+  bool march = k.los_mode == 1;
+  size_t lds = step_lds_bytes(h, march);
+  dim3 grid((h->E + WAVE - 1) / WAVE), block(WAVE);
+  hipStream_t st = (hipStream_t)stream;
+  if (march)
+    step_kernel<true><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev,
+                                               obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
+  else
+    step_kernel<false><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev,
+                                                obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_red_dev, void *stream) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  if (agent >= h->A || agent < LNW_OBS_RED) return fail(LNW_EINVAL, "bad agent selector");
+  KState s = make_state(h);
+  bool march = h->kp.los_mode == 1;
+  size_t lds = step_lds_bytes(h, march);
+  dim3 grid((h->E + WAVE - 1) / WAVE), block(WAVE);
+  hipStream_t st = (hipStream_t)stream;
+  if (march)
+    observe_kernel<true><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
+  else
+    observe_kernel<false><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbytes) {
+  if (!h || !dev_ptr || !nbytes) return fail(LNW_EINVAL, "null argument");
+  const int64_t E = h->E, A = h->A;
+  switch (field) {
+    case LNW_F_POS: *dev_ptr = h->pos; *nbytes = 4 * A * E; break;
+    case LNW_F_RADAR: *dev_ptr = h->radar; *nbytes = 4 * A * E; break;
+    case LNW_F_MISSILES: *dev_ptr = h->miss; *nbytes = A * E; break;
+    case LNW_F_MKIND: *dev_ptr = h->mkind; *nbytes = A * E; break;
+    case LNW_F_ALIVE: *dev_ptr = h->alive; *nbytes = A * E; break;
+    case LNW_F_TYPE: *dev_ptr = h->type; *nbytes = A * E; break;
+    case LNW_F_STEPS: *dev_ptr = h->steps; *nbytes = 4 * A * E; break;
+    case LNW_F_DIST_LZ: *dev_ptr = h->dist_lz; *nbytes = 8 * A * E; break;
+    case LNW_F_TL_CNT: *dev_ptr = h->tl_cnt; *nbytes = 2 * A * E; break;
+    case LNW_F_TL: *dev_ptr = h->tl; *nbytes = 2 * A * h->T * E; break;
+    case LNW_F_DUCT: *dev_ptr = h->duct; *nbytes = 8 * E; break;
+    case LNW_F_ENV: *dev_ptr = h->envi; *nbytes = 4 * 8 * E; break;
+    case LNW_F_RNG: *dev_ptr = h->rng; *nbytes = 8 * E; break;
+    case LNW_F_ERR: *dev_ptr = h->err; *nbytes = 4 * E; break;
+    default: return fail(LNW_EINVAL, "unknown state field");
+  }
+  return 0;
+}
+
+int lnw_tlist_cap(lnw_handle *h) { return h ? h->T : LNW_EINVAL; }
+
+int lnw_los_batch(const uint8_t *grid_dev, int32_t G, const int16_t *pairs_dev, int64_t n,
+                  int32_t move_thr, int32_t ew_thr, uint8_t *out_dev, void *stream) {
+  if (!grid_dev || !pairs_dev || !out_dev) return fail(LNW_EINVAL, "null argument");
+  if (n <= 0) return 0;
+  los_batch_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      grid_dev, G, pairs_dev, n, move_thr, ew_thr, out_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_astar_batch(const uint8_t *grid_dev, int32_t G, int32_t move_thr, const int8_t *types_dev,
+                    const int16_t *start_dev, const int16_t *target_dev, int64_t n,
+                    int16_t *plen_dev, int8_t *kind_dev, uint8_t *feasible_dev, void *stream) {
+  if (!grid_dev || !types_dev || !start_dev || !target_dev || !plen_dev || !kind_dev || !feasible_dev)
+    return fail(LNW_EINVAL, "null argument");
+  if (n <= 0) return 0;
+  astar_batch_kernel<<<(unsigned)((n + WAVE - 1) / WAVE), WAVE, 0, (hipStream_t)stream>>>(
+      grid_dev, G, move_thr, types_dev, start_dev, target_dev, n, plen_dev, kind_dev, feasible_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_move_batch(lnw_handle *h, const int8_t *types_dev, const int16_t *pos_dev,
+                   const double *act_dev, const uint8_t *is_f32_dev, int64_t n, int32_t *rounded_dev,
+                   uint8_t *ok_dev, void *stream) {
+  if (!h || !types_dev || !pos_dev || !act_dev || !is_f32_dev || !rounded_dev || !ok_dev)
+    return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  if (n <= 0) return 0;
+  KState s = make_state(h);
+  move_batch_kernel<<<(unsigned)((n + WAVE - 1) / WAVE), WAVE, 0, (hipStream_t)stream>>>(
+      h->kp, s, types_dev, pos_dev, act_dev, is_f32_dev, n, rounded_dev, ok_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_path_query(lnw_handle *h, const int8_t *types_dev, const int16_t *start_dev,
+                   const int16_t *target_dev, int64_t n, uint8_t *out_dev, void *stream) {
+  if (!h || !types_dev || !start_dev || !target_dev || !out_dev) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  if (n <= 0) return 0;
+  KState s = make_state(h);
+  path_query_kernel<<<(unsigned)((n + WAVE - 1) / WAVE), WAVE, 0, (hipStream_t)stream>>>(
+      h->kp, s, types_dev, start_dev, target_dev, n, out_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_los_query(lnw_handle *h, const int16_t *pairs_dev, int64_t n, uint8_t *out_dev, void *stream) {
+  if (!h || !pairs_dev || !out_dev) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  if (n <= 0) return 0;
+  KState s = make_state(h);
+  los_query_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(h->kp, s, pairs_dev, n, out_dev);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int lnw_copy(void *dst, const void *src, int64_t nbytes, void *stream) {
+  if (nbytes <= 0) return 0;
+  if (!dst || !src) return fail(LNW_EINVAL, "null argument");
+  HIPCHK(hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDefault, (hipStream_t)stream));
+  return 0;
+}
+
+int lnw_fill_uniform_f32(float *out_dev, int64_t n, uint64_t seed, uint64_t offset, void *stream) {
+  if (!out_dev) return fail(LNW_EINVAL, "null argument");
+  if (n <= 0) return 0;
+  if (offset & 3) return fail(LNW_EINVAL, "offset must be a multiple of 4");
+  long long nt = (n + 3) / 4;
+  fill_uniform_kernel<<<(unsigned)((nt + 255) / 256), 256, 0, (hipStream_t)stream>>>(out_dev, n, seed, offset);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

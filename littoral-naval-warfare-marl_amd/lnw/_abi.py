@@ -1,0 +1,97 @@
+"""ctypes binding of liblnw.so (include/lnw.h).
+
+The product path: every call goes to the HIP library built in-tree for gfx950.
+There is no CPU fallback — if the library is missing or fails to load, the
+import raises.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblnw.so")
+
+LNW_SMALL, LNW_LARGE, LNW_LS = 0, 1, 2
+LNW_ACT_F32, LNW_ACT_F64, LNW_ACT_I32 = 0, 1, 2
+LNW_KIND_PYFLOAT, LNW_KIND_F32, LNW_KIND_F64 = 1, 2, 3
+LNW_RNG_PHILOX, LNW_RNG_TAPE = 0, 1
+LNW_OBS_ALL, LNW_OBS_BLUE, LNW_OBS_RED = -1, -2, -3
+LNW_ERRF_ZERODIV, LNW_ERRF_NAN_ROUND, LNW_ERRF_TAPE, LNW_ERRF_MISSILES = 1, 2, 4, 8
+
+(F_POS, F_RADAR, F_MISSILES, F_MKIND, F_ALIVE, F_TYPE, F_STEPS, F_DIST_LZ, F_TL_CNT, F_TL,
+ F_DUCT, F_ENV, F_RNG, F_ERR) = range(14)
+
+# exported symbols (must match include/lnw.h)
+SYMBOLS = [
+    "lnw_abi_version", "lnw_last_error", "lnw_create", "lnw_destroy", "lnw_load_terrain",
+    "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_state_field", "lnw_tlist_cap",
+    "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
+    "lnw_fill_uniform_f32", "lnw_hit_tables",
+]
+
+
+class Params(C.Structure):
+    _fields_ = [("discrete", C.c_int32), ("landing_ops", C.c_int32), ("aggressive", C.c_int32),
+                ("side_blue", C.c_int32), ("trained_red", C.c_int32), ("move_thr", C.c_int32),
+                ("ew_thr", C.c_int32), ("lz_x", C.c_int32), ("lz_y", C.c_int32),
+                ("red_aggression", C.c_double), ("episode_steps", C.c_int32),
+                ("auto_reset", C.c_int32), ("los_mode", C.c_int32), ("move_mode", C.c_int32)]
+
+
+class Spawn(C.Structure):
+    _fields_ = [("types", C.c_int32 * 64), ("pos", (C.c_int32 * 2) * 64),
+                ("rand_ls", C.c_int32 * 64), ("box_lo", C.c_int32 * 2),
+                ("box_hi", C.c_int32 * 2)]
+
+
+class LnwError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load liblnw.so (raises if it is missing: no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("LNW_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise LnwError(f"liblnw.so not built at {path}; run lnw.build.build() "
+                       "(or __graft_entry__.build())")
+    L = C.CDLL(path)
+    P, I32, I64, U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+    sig = {
+        "lnw_abi_version": ([], C.c_int),
+        "lnw_last_error": ([], C.c_char_p),
+        "lnw_create": ([C.POINTER(Params), I32, I32, I32, I32, I64, C.POINTER(P)], C.c_int),
+        "lnw_destroy": ([P], C.c_int),
+        "lnw_load_terrain": ([P, P, I32], C.c_int),
+        "lnw_set_rng": ([P, I32, U64, P, P], C.c_int),
+        "lnw_reset": ([P, P, C.POINTER(Spawn), P, P], C.c_int),
+        "lnw_step": ([P, P, I32, P, P, P, P, P, P, P, P], C.c_int),
+        "lnw_observe": ([P, I32, P, P, P], C.c_int),
+        "lnw_state_field": ([P, I32, C.POINTER(P), C.POINTER(I64)], C.c_int),
+        "lnw_tlist_cap": ([P], C.c_int),
+        "lnw_los_batch": ([P, I32, P, I64, I32, I32, P, P], C.c_int),
+        "lnw_astar_batch": ([P, I32, I32, P, P, P, I64, P, P, P, P], C.c_int),
+        "lnw_move_batch": ([P, P, P, P, P, I64, P, P, P], C.c_int),
+        "lnw_path_query": ([P, P, P, P, I64, P, P], C.c_int),
+        "lnw_los_query": ([P, P, I64, P, P], C.c_int),
+        "lnw_copy": ([P, P, I64, P], C.c_int),
+        "lnw_fill_uniform_f32": ([P, I64, U64, U64, P], C.c_int),
+        "lnw_hit_tables": ([P, P], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = _lib.lnw_last_error().decode() if _lib is not None else "?"
+        raise LnwError(f"lnw call failed ({rc}): {msg}")
+    return rc

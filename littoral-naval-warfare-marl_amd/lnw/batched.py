@@ -1,0 +1,231 @@
+"""BatchedGame: E independent reference games stepped together on one MI355X.
+
+Host side of the drop-in boundary: PyTorch-ROCm tensors for the caller-owned
+buffers (actions, observations, rewards) and the C-ABI (include/lnw.h) for
+everything else. One instance = one lnw handle = one device (one process per
+GPU for multi-GPU; shard envs by global id, see lnw.shard).
+
+Reference correspondence (valauri/Littoral-Naval-Warfare-MARL):
+  reset()    Game.reset            game.py:528-613
+  step()     Game.step             game.py:298-525
+  observe()  Combatant.get_obs     combatant.py:90-233 (side effects included)
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import (F_ALIVE, F_DIST_LZ, F_DUCT, F_ENV, F_ERR, F_MISSILES, F_MKIND, F_POS,
+                   F_RADAR, F_RNG, F_STEPS, F_TL, F_TL_CNT, F_TYPE, LNW_ACT_F32, LNW_ACT_F64,
+                   LNW_ACT_I32, LNW_LARGE, LNW_LS, LNW_RNG_PHILOX, LNW_RNG_TAPE, LNW_SMALL, Spawn,
+                   check)
+from .config import Scenario
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+TYPE_CODES = {"small": LNW_SMALL, "large": LNW_LARGE, "ls": LNW_LS}
+
+# field -> (torch dtype of the raw bytes, shape builder)
+_FIELDS = {
+    F_POS: (torch.int32, lambda g: (g.A, g.E)),
+    F_RADAR: (torch.int32, lambda g: (g.A, g.E)),
+    F_MISSILES: (torch.uint8, lambda g: (g.A, g.E)),
+    F_MKIND: (torch.uint8, lambda g: (g.A, g.E)),
+    F_ALIVE: (torch.uint8, lambda g: (g.A, g.E)),
+    F_TYPE: (torch.uint8, lambda g: (g.A, g.E)),
+    F_STEPS: (torch.int32, lambda g: (g.A, g.E)),
+    F_DIST_LZ: (torch.float64, lambda g: (g.A, g.E)),
+    F_TL_CNT: (torch.int16, lambda g: (g.A, g.E)),
+    F_TL: (torch.int16, lambda g: (g.A, g.T, g.E)),
+    F_DUCT: (torch.float64, lambda g: (g.E,)),
+    F_ENV: (torch.int32, lambda g: (8, g.E)),
+    F_RNG: (torch.int64, lambda g: (g.E,)),
+    F_ERR: (torch.int32, lambda g: (g.E,)),
+}
+ENV_KEYS = ["n_blue_left", "n_red_left", "steps_done", "blue_victory", "red_victory",
+            "blue_engagements", "red_engagements", "episode"]
+
+
+def default_grid(G=100):
+    """The reference's terrain: balt_mod_400x400_2.png -> LANCZOS resize -> L
+    (game.py:616-626), committed as data at G=100 and G=200."""
+    return np.load(os.path.join(DATA, f"baltic_grid{G}.npy"))
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class BatchedGame:
+    def __init__(self, n_envs, blue_types, red_types, scenario=None, device=0, env_id_base=0,
+                 grid=None, seed=0):
+        self.L = _abi.load()
+        self.sc = scenario or Scenario()
+        self.E = int(n_envs)
+        self.blue_types = [TYPE_CODES.get(t, t) for t in blue_types]
+        self.red_types = [TYPE_CODES.get(t, t) for t in red_types]
+        self.nb, self.nr = len(self.blue_types), len(self.red_types)
+        self.A = self.nb + self.nr
+        self.Db, self.Dr = 4 * self.nb + 52, 4 * self.nr + 52
+        self.device = torch.device("cuda", device)
+        self.env_id_base = int(env_id_base)
+        self._params = self.sc.params()
+        h = C.c_void_p()
+        check(self.L.lnw_create(C.byref(self._params), self.E, self.nb, self.nr, device,
+                                self.env_id_base, C.byref(h)))
+        self.h = h
+        self.T = self.L.lnw_tlist_cap(self.h)
+        self.grid = np.ascontiguousarray(default_grid(100) if grid is None else grid, np.uint8)
+        self.G = self.grid.shape[0]
+        check(self.L.lnw_load_terrain(self.h, self.grid.ctypes.data_as(C.c_void_p), self.G))
+        self._tape = None
+        self.set_rng(seed)
+        dev = self.device
+        self.obs_blue = torch.zeros((self.E, self.nb, self.Db), dtype=torch.float32, device=dev)
+        self.obs_red = torch.zeros((self.E, self.nr, self.Dr), dtype=torch.float32, device=dev)
+        self.rew_blue = torch.zeros((self.E, self.nb), dtype=torch.float32, device=dev)
+        self.rew_red = torch.zeros((self.E, self.nr), dtype=torch.float32, device=dev)
+        self.done = torch.ones((self.E,), dtype=torch.int32, device=dev)
+        self.cog = torch.zeros((self.E,), dtype=torch.float32, device=dev)
+        self._spawn = None
+
+    # ---------------------------------------------------------------- rng
+    def set_rng(self, seed):
+        """Production RNG: Philox4x32-10 keyed by (seed, global env id)."""
+        self._tape = None
+        check(self.L.lnw_set_rng(self.h, LNW_RNG_PHILOX, int(seed) & (2**64 - 1), None, None))
+
+    def set_tape(self, tape, offsets):
+        """Parity RNG: env e consumes tape[offsets[e]:offsets[e+1]] in call order."""
+        tape = torch.as_tensor(tape, dtype=torch.float64).to(self.device).contiguous()
+        offs = torch.as_tensor(offsets, dtype=torch.int64).to(self.device).contiguous()
+        assert offs.numel() == self.E + 1
+        self._tape = (tape, offs)
+        check(self.L.lnw_set_rng(self.h, LNW_RNG_TAPE, 0, _ptr(tape), _ptr(offs)))
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # -------------------------------------------------------------- reset
+    def reset(self, positions=None, rand_ls=None, env_mask=None, pos_per_env=None, box=None):
+        """Game.reset for the masked envs (all by default). positions: A (x, y)
+        spawn cells (blue then red); rand_ls: A flags drawing the LandingShip
+        spawn (game.py:587-591); pos_per_env: [E, A, 2] int32 tensor; box:
+        ((x0, y0), (x1, y1)) random-water-cell spawn box."""
+        sp = Spawn()
+        types = self.blue_types + self.red_types
+        for a, t in enumerate(types):
+            sp.types[a] = int(t)
+        if positions is not None:
+            for a, (x, y) in enumerate(positions):
+                sp.pos[a][0], sp.pos[a][1] = int(x), int(y)
+        if rand_ls is not None:
+            for a, f in enumerate(rand_ls):
+                sp.rand_ls[a] = int(bool(f))
+        if box is not None:
+            (x0, y0), (x1, y1) = box
+            sp.box_lo[0], sp.box_lo[1], sp.box_hi[0], sp.box_hi[1] = x0, y0, x1, y1
+        self._spawn = sp
+        mask = None
+        if env_mask is not None:
+            mask = torch.as_tensor(env_mask, dtype=torch.uint8, device=self.device).contiguous()
+        pe = None
+        if pos_per_env is not None:
+            pe = torch.as_tensor(pos_per_env, dtype=torch.int32, device=self.device).contiguous()
+            self._pos_per_env = pe
+        check(self.L.lnw_reset(self.h, _ptr(mask), C.byref(sp), _ptr(pe), self._stream()))
+        if mask is not None or pe is not None:
+            torch.cuda.current_stream(self.device).synchronize()
+
+    # --------------------------------------------------------------- step
+    def step(self, actions, row_kind=None):
+        """Game.step for all envs. actions: [E, A, 4] float32 / float64 tensor
+        (continuous) or int32 (discrete). Mutated in place where the reference
+        mutates its action rows (game.py:379). Returns the output tensors."""
+        a = actions
+        assert a.is_cuda and a.is_contiguous() and tuple(a.shape) == (self.E, self.A, 4)
+        if a.dtype == torch.float32:
+            dt = LNW_ACT_F32
+        elif a.dtype == torch.float64:
+            dt = LNW_ACT_F64
+        elif a.dtype == torch.int32:
+            dt = LNW_ACT_I32
+        else:
+            raise TypeError(f"unsupported action dtype {a.dtype}")
+        rk = None
+        if row_kind is not None:
+            rk = torch.as_tensor(row_kind, dtype=torch.uint8, device=self.device).contiguous()
+        check(self.L.lnw_step(self.h, _ptr(a), dt, _ptr(rk), _ptr(self.obs_blue),
+                              _ptr(self.obs_red), _ptr(self.rew_blue), _ptr(self.rew_red),
+                              _ptr(self.done), _ptr(self.cog), self._stream()))
+        return dict(obs_blue=self.obs_blue, obs_red=self.obs_red, rew_blue=self.rew_blue,
+                    rew_red=self.rew_red, done=self.done, cog=self.cog)
+
+    def observe(self, agent=-1):
+        """ship.get_obs() for every live ship (agent=-1, blue then red), one side
+        (-2 blue, -3 red) or one agent index, in every env."""
+        check(self.L.lnw_observe(self.h, int(agent), _ptr(self.obs_blue), _ptr(self.obs_red),
+                                 self._stream()))
+        return self.obs_blue, self.obs_red
+
+    # -------------------------------------------------------------- state
+    def _field(self, f):
+        p = C.c_void_p()
+        n = C.c_int64()
+        check(self.L.lnw_state_field(self.h, f, C.byref(p), C.byref(n)))
+        return p, n.value
+
+    def get(self, f):
+        dt, shp = _FIELDS[f]
+        p, n = self._field(f)
+        out = torch.empty(shp(self), dtype=dt, device=self.device)
+        assert out.numel() * out.element_size() == n
+        check(self.L.lnw_copy(_ptr(out), p, n, self._stream()))
+        return out
+
+    def set(self, f, value):
+        dt, shp = _FIELDS[f]
+        p, n = self._field(f)
+        v = torch.as_tensor(value).to(device=self.device, dtype=dt).reshape(shp(self)).contiguous()
+        check(self.L.lnw_copy(p, _ptr(v), n, self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def agents(self):
+        """Per-agent state as numpy arrays shaped [E, A] (host copy)."""
+        pos = self.get(F_POS).cpu().numpy().astype(np.int64)
+        out = dict(x=(pos & 0x7fff).T, y=((pos >> 16) & 0x7fff).T,
+                   radar=self.get(F_RADAR).cpu().numpy().T,
+                   missiles=self.get(F_MISSILES).cpu().numpy().T,
+                   mkind=self.get(F_MKIND).cpu().numpy().T,
+                   alive=self.get(F_ALIVE).cpu().numpy().T,
+                   type=self.get(F_TYPE).cpu().numpy().T,
+                   steps_done=self.get(F_STEPS).cpu().numpy().T,
+                   dist_lz=self.get(F_DIST_LZ).cpu().numpy().T,
+                   tl_cnt=self.get(F_TL_CNT).cpu().numpy().T.astype(np.int64))
+        return out
+
+    def env_state(self):
+        e = self.get(F_ENV).cpu().numpy()
+        d = {k: e[i] for i, k in enumerate(ENV_KEYS)}
+        d["ducting"] = self.get(F_DUCT).cpu().numpy()
+        d["rng"] = self.get(F_RNG).cpu().numpy()
+        d["err"] = self.get(F_ERR).cpu().numpy()
+        return d
+
+    def tlists(self, env):
+        """Target lists of one env: list (per agent) of (x, y) tuples."""
+        cnt = self.get(F_TL_CNT).cpu().numpy().astype(np.int64)[:, env]
+        tl = self.get(F_TL).cpu().numpy().astype(np.int64)[:, :, env] & 0xffff
+        return [[(int(v & 0xff), int(v >> 8)) for v in tl[a, :cnt[a]]] for a in range(self.A)]
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.L.lnw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

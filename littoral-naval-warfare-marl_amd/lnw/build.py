@@ -1,0 +1,50 @@
+"""Build liblnw.so in-tree for gfx950 with hipcc (no JIT cache, no CPU path).
+
+-ffp-contract=off keeps every float/double operation un-fused so the kernels
+round exactly like CPython/NumPy (the reference); see DESIGN.md "Numerics".
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+OUT = os.path.join(HERE, "liblnw.so")
+SOURCES = [os.path.join(CSRC, "lnw_kernels.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, "lnw_device.h"), os.path.join(INCLUDE, "lnw.h")]
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def flags(arch="gfx950"):
+    return [f"--offload-arch={arch}", "-O3", "-std=c++17", "-ffp-contract=off",
+            "-fno-gpu-flush-denormals-to-zero", "-fPIC", "-shared", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def build(force=False, verbose=False):
+    if not force and os.path.exists(OUT):
+        t = os.path.getmtime(OUT)
+        if all(os.path.getmtime(d) <= t for d in DEPS):
+            return OUT
+    cmd = [hipcc()] + flags() + SOURCES + ["-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("hipcc failed building liblnw.so")
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))
