@@ -46,6 +46,7 @@ struct KParams {
   double den[2];      // aggressive-reward denominator per mast class (game.py:269)
   double det_q[2];    // detected_prob: [0] target radar==1 (0.345-0.1), [1] otherwise
   int box_lo[2], box_hi[2];
+  int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M
 };
 
 // Device state (SoA, agent-major [field][agent][env] so a wave of envs reads
@@ -68,6 +69,7 @@ struct KState {
   double *bear_val;    // [nmax*nmax][E] EW bearing scratch
   uint8_t *bear_ship;  // [nmax*nmax][E]
   const uint8_t *grid;     // [G][G]
+  const float *gridf;      // [G][G] grid/255 as float32 (observation windows)
   const uint32_t *mask2;   // [G][W16] 2 bits per cell: bit0 > move_thr, bit1 > ew_thr
   const uint32_t *mvtab;   // [2][G*G][3]
   const uint32_t *lostab;  // [G*G][486]

@@ -16,6 +16,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -34,33 +35,48 @@ constexpr int PADB = WAVE + 4;  // byte-array stride
 // per-wave LDS carve-up for the step/observe kernels
 // ---------------------------------------------------------------------------
 struct LdsLayout {
-  int pos_cur, pos_old, pos_new, radar_cur, radar_old, reward;        // word/dword offsets (bytes)
-  int miss_cur, miss_old, mkind, type, alive0, eng, tcnt, obsd;       // byte arrays
-  int observed, bcnt, border, open, mask, total;
+  // persistent through phase O
+  int pos_cur, pos_old, radar_cur, radar_old, tcnt, miss_cur, miss_old, type, alive0, obsd;
+  // phase-S scratch (dead before phase O) ...
+  int pos_new, reward, observed, open, mkind, eng, bcnt, border;
+  // ... aliased by the phase-O row staging area
+  int stage, mask, total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int A, int nmax, int mask_words) {
+// Row staging for phase O: up to 64 observation rows of D+1 floats (odd stride
+// -> conflict-free ds_write_b32 across lanes).
+__host__ __device__ inline int stage_bytes(int A, int nb, int nr) {
+  int epg = WAVE / A;
+  return epg * (nb * (4 * nb + 53) + nr * (4 * nr + 53)) * 4;
+}
+
+__host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax, int mask_words) {
   LdsLayout L;
   int o = 0;
   L.pos_cur = o; o += A * PAD * 4;
   L.pos_old = o; o += A * PAD * 4;
-  L.pos_new = o; o += A * PAD * 4;
   L.radar_cur = o; o += A * PAD * 4;
   L.radar_old = o; o += A * PAD * 4;
-  o = (o + 7) & ~7;
-  L.reward = o; o += A * PAD * 8;
   L.tcnt = o; o += A * PAD * 4;
-  L.observed = o; o += nmax * PAD * 4;
-  L.open = o; o += OPEN_CAP * WAVE * 4;
   L.miss_cur = o; o += A * PADB;
   L.miss_old = o; o += A * PADB;
-  L.mkind = o; o += A * PADB;
   L.type = o; o += A * PADB;
   L.alive0 = o; o += A * PADB;
-  L.eng = o; o += A * PADB;
   L.obsd = o; o += A * PADB;
+  o = (o + 15) & ~15;
+  const int scratch = o;
+  L.stage = scratch;
+  L.pos_new = o; o += A * PAD * 4;
+  o = (o + 7) & ~7;
+  L.reward = o; o += A * PAD * 8;
+  L.observed = o; o += nmax * PAD * 4;
+  L.open = o; o += OPEN_CAP * WAVE * 4;
+  L.mkind = o; o += A * PADB;
+  L.eng = o; o += A * PADB;
   L.bcnt = o; o += nmax * PADB;
   L.border = o; o += nmax * PADB;
+  int st_end = scratch + stage_bytes(A, nb, nr);
+  if (st_end > o) o = st_end;
   o = (o + 15) & ~15;
   L.mask = o; o += mask_words * 4;
   L.total = o;
@@ -73,6 +89,7 @@ struct Cols {
   double *reward;
   uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border;
   uint32_t *mask;
+  float *stage;
 };
 
 __device__ inline Cols carve(char *base, const LdsLayout &L) {
@@ -96,6 +113,7 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
   c.bcnt = (uint8_t *)(base + L.bcnt);
   c.border = (uint8_t *)(base + L.border);
   c.mask = (uint32_t *)(base + L.mask);
+  c.stage = (float *)(base + L.stage);
   return c;
 }
 
@@ -525,69 +543,110 @@ __device__ inline Rng make_rng(const KParams &P, const KState &S, int env) {
 
 // ---------------------------------------------------------------------------
 // phase O: observation vectors (combatant.py:163-233, landingship.py:167-239)
+// One lane per (env, agent) row builds its D floats into a padded LDS row; the
+// wave then copies each side's block ([envs][n][D], contiguous in the output)
+// out with consecutive lanes on consecutive floats (256-B coalesced stores).
 // ---------------------------------------------------------------------------
-__device__ void write_obs(const KParams &P, const KState &S, Cols &c, const double *duct_col,
-                          int side, float *out, int env0, int nenv, bool only_observed) {
-  const int lane = threadIdx.x;
-  const int ns = side ? P.nr : P.nb;
+__device__ void build_row(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
+                          int el, int k, float *row, bool only_observed) {
+  const int side = k >= P.nb;
   const int own0 = side ? P.nb : 0;
+  const int ns = side ? P.nr : P.nb;
+  const int kl = k - own0;
   const int D = 4 * ns + 52;
-  const int Bs = ns * D;
   const int G = P.G;
-  for (int base = 0; base < Bs; base += WAVE) {
-    const int r = base + lane;
-    const bool valid = r < Bs;
-    const int kl = valid ? r / D : 0;
-    const int d = valid ? r - kl * D : 0;
-    const int k = own0 + kl;
-    for (int el = 0; el < nenv; el++) {
-      float v = 0.0f;
-      if (valid && c.alive0[k * PADB + el] && (!only_observed || c.obsd[k * PADB + el])) {
-        const int tk = c.type[k * PADB + el];
-        const int Wn = tk == T_LS ? 25 : 49;
-        if (d < Wn) {
-          uint32_t p = c.pos_cur[k * PAD + el];
-          int x, y;
-          if (tk == T_LS) { x = pos_x(p) - 1 + d / 5; y = pos_y(p) - 1 + d % 5; }
-          else { x = pos_x(p) - 3 + d / 7; y = pos_y(p) - 3 + d % 7; }
-          if (0 <= x && x < 100 && 0 <= y && y < 100)
-            v = (float)((double)S.grid[x * G + y] / 255.0);
-        } else {
-          const int t = d - Wn;
-          if (t < 4) {
-            uint32_t p = c.pos_cur[k * PAD + el];
-            if (t == 0) v = (float)((double)pos_x(p) / (double)G);
-            else if (t == 1) v = (float)((double)pos_y(p) / (double)G);
-            else if (t == 2) v = (float)c.radar_cur[k * PAD + el];
-            else v = (float)((double)c.miss_cur[k * PADB + el] / miss_norm(tk));
-          } else if (t < 4 * ns) {
-            int j = (t - 4) >> 2, f = (t - 4) & 3;
-            int il = j < kl ? j : j + 1;
-            int i = own0 + il;
-            if (c.alive0[i * PADB + el]) {
-              bool nw = il <= kl;
-              int ti = c.type[i * PADB + el];
-              if (f < 2) {
-                uint32_t p = nw ? c.pos_cur[i * PAD + el] : c.pos_old[i * PAD + el];
-                v = (float)((double)(f == 0 ? pos_x(p) : pos_y(p)) / (double)G);
-              } else if (f == 2) {
-                v = (float)(nw ? c.radar_cur[i * PAD + el] : c.radar_old[i * PAD + el]);
-              } else {
-                int m = nw ? c.miss_cur[i * PADB + el] : c.miss_old[i * PADB + el];
-                v = (float)((double)m / miss_norm(ti));
-              }
-            }
-          } else if (t == 4 * ns) {
-            v = (float)c.tcnt[k * PAD + el];
-          } else if (t == 4 * ns + 1) {
-            v = tk == T_LS ? 1.0f : 0.0f;
-          } else if (t == 4 * ns + 2) {
-            v = (float)(duct_col[el] / 2.0);
-          }
-        }
+  if (!c.alive0[k * PADB + el] || (only_observed && !c.obsd[k * PADB + el])) {
+    for (int d = 0; d < D; d++) row[d] = 0.0f;
+    return;
+  }
+  const int tk = c.type[k * PADB + el];
+  const uint32_t p = c.pos_cur[k * PAD + el];
+  const int px = pos_x(p), py = pos_y(p);
+  int idx;
+  if (tk == T_LS) {
+    // asymmetric 5x5 window rows/cols pos-1..pos+3 (landingship.py:178-188)
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      const int x = px - 1 + i;
+#pragma unroll
+      for (int j = 0; j < 5; j++) {
+        const int y = py - 1 + j;
+        row[i * 5 + j] = (0 <= x && x < 100 && 0 <= y && y < 100) ? S.gridf[x * G + y] : 0.0f;
       }
-      if (valid) out[(size_t)(env0 + el) * Bs + r] = v;
     }
+    idx = 25;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      const int x = px - 3 + i;
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+        const int y = py - 3 + j;
+        row[i * 7 + j] = (0 <= x && x < 100 && 0 <= y && y < 100) ? S.gridf[x * G + y] : 0.0f;
+      }
+    }
+    idx = 49;
+  }
+  row[idx++] = (float)((double)px / (double)G);
+  row[idx++] = (float)((double)py / (double)G);
+  row[idx++] = (float)c.radar_cur[k * PAD + el];
+  row[idx++] = (float)((double)c.miss_cur[k * PADB + el] / miss_norm(tk));
+  for (int il = 0; il < ns; il++) {
+    if (il == kl) continue;
+    const int i = own0 + il;
+    if (c.alive0[i * PADB + el]) {
+      // own ships that acted before k this step show their new state
+      const bool nw = il < kl;
+      const uint32_t q = nw ? c.pos_cur[i * PAD + el] : c.pos_old[i * PAD + el];
+      row[idx] = (float)((double)pos_x(q) / (double)G);
+      row[idx + 1] = (float)((double)pos_y(q) / (double)G);
+      row[idx + 2] = (float)(nw ? c.radar_cur[i * PAD + el] : c.radar_old[i * PAD + el]);
+      const int m = nw ? c.miss_cur[i * PADB + el] : c.miss_old[i * PADB + el];
+      row[idx + 3] = (float)((double)m / miss_norm(c.type[i * PADB + el]));
+    } else {
+      row[idx] = row[idx + 1] = row[idx + 2] = row[idx + 3] = 0.0f;
+    }
+    idx += 4;
+  }
+  row[idx++] = (float)c.tcnt[k * PAD + el];
+  row[idx++] = tk == T_LS ? 1.0f : 0.0f;
+  row[idx++] = (float)(duct_col[el] / 2.0);
+  for (; idx < D; idx++) row[idx] = 0.0f;
+}
+
+__device__ inline void copy_side(const float *stage, float *out, int ns, int ne, long long genv0) {
+  if (!out) return;
+  const int lane = threadIdx.x;
+  const int D = 4 * ns + 52;
+  const int n = ne * ns * D;
+  float *base = out + (size_t)genv0 * ns * D;
+  int row = lane / D, col = lane - (lane / D) * D;
+  for (int i = lane; i < n; i += WAVE) {
+    base[i] = stage[row * (D + 1) + col];
+    col += WAVE;
+    while (col >= D) { col -= D; row++; }
+  }
+}
+
+__device__ void write_obs(const KParams &P, const KState &S, Cols &c, const double *duct_col,
+                          float *obs_b, float *obs_r, int env0, int nenv, bool only_observed) {
+  const int lane = threadIdx.x;
+  const int A = P.A, nb = P.nb, nr = P.nr;
+  const int epg = WAVE / A;
+  const int my_e = lane / A, my_k = lane - (lane / A) * A;
+  const int side = my_k >= nb;
+  const int kl = side ? my_k - nb : my_k;
+  const int ns = side ? nr : nb;
+  float *stage_b = c.stage;
+  float *stage_r = c.stage + epg * nb * (4 * nb + 53);
+  float *row = (side ? stage_r : stage_b) + (my_e * ns + kl) * (4 * ns + 53);
+  for (int g0 = 0; g0 < nenv; g0 += epg) {
+    const int ne = (nenv - g0) < epg ? (nenv - g0) : epg;
+    if (my_e < ne) build_row(P, S, c, duct_col, g0 + my_e, my_k, row, only_observed);
+    __syncthreads();
+    copy_side(stage_b, obs_b, nb, ne, env0 + g0);
+    copy_side(stage_r, obs_r, nr, ne, env0 + g0);
+    __syncthreads();
   }
 }
 
@@ -610,11 +669,11 @@ __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, in
       uint8_t m = S.miss[ai];
       COLB(c.miss_cur, a) = m;
       COLB(c.miss_old, a) = m;
-      COLB(c.mkind, a) = S.mkind[ai];
       COLB(c.type, a) = S.type[ai];
       COLB(c.alive0, a) = S.alive[ai];
       COLW(c.tcnt, a) = S.tl_cnt[ai];
       COLB(c.eng, a) = 0;
+      COLB(c.mkind, a) = S.mkind[ai];
       COLB(c.obsd, a) = 0;
     } else {
       COLB(c.alive0, a) = 0;
@@ -640,7 +699,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   const bool valid = env < E;
   const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
   const int A = P.A, nb = P.nb, nr = P.nr;
-  LdsLayout L = lds_layout(A, S.nmax, MARCH ? P.G * P.W16 : 0);
+  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, MARCH ? P.G * P.W16 : 0);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
 
@@ -656,7 +715,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
 
   // ---- phase M: movement feasibility for every agent of this env --------
   const int dt = P.act_dtype;
-  if (valid) {
+  if (valid && !(P.dbg_skip & 4)) {
     for (int a = 0; a < A; a++) {
       if (!COLB(c.alive0, a)) continue;
       uint32_t p = COLW(c.pos_old, a);
@@ -704,7 +763,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   // ---- phase S: sequential agent loop ------------------------------------
   int done = 1;
   float cog = NAN;
-  if (valid) {
+  if (valid && !(P.dbg_skip & 2)) {
     Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E};
     Neut N{{0, 0}, {0u, 0u}};
     int hits[2] = {0, 0};
@@ -876,8 +935,8 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   }
   __syncthreads();
   // ---- phase O: observations ---------------------------------------------
-  if (obs_b) write_obs(P, S, c, duct_col, 0, obs_b, env0, nenv, false);
-  if (obs_r) write_obs(P, S, c, duct_col, 1, obs_r, env0, nenv, false);
+  if (P.dbg_skip & 1) return;
+  write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -893,7 +952,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   const bool valid = env < E;
   const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
   const int A = P.A, nb = P.nb;
-  LdsLayout L = lds_layout(A, S.nmax, MARCH ? P.G * P.W16 : 0);
+  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, MARCH ? P.G * P.W16 : 0);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
   const uint32_t *mask = S.mask2;
@@ -922,8 +981,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   }
   __syncthreads();
   // rows of ships not observed in this call are written as zeros
-  if (obs_b) write_obs(P, S, c, duct_col, 0, obs_b, env0, nenv, true);
-  if (obs_r) write_obs(P, S, c, duct_col, 1, obs_r, env0, nenv, true);
+  write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, true);
 }
 
 __global__ void reset_kernel(KParams P, KState S, const uint8_t *mask) {
@@ -1143,6 +1201,7 @@ struct lnw_handle {
   bool terrain = false;
   // device buffers
   uint8_t *d_grid = nullptr;
+  float *d_gridf = nullptr;
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -1177,7 +1236,7 @@ KState make_state(lnw_handle *h) {
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
   s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
-  s.grid = h->d_grid; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.grid = h->d_grid; s.gridf = h->d_gridf; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
   s.sp_pos_env = nullptr;
@@ -1186,7 +1245,7 @@ KState make_state(lnw_handle *h) {
 }
 
 size_t step_lds_bytes(const lnw_handle *h, bool march) {
-  LdsLayout L = lds_layout(h->A, h->nmax, march ? h->G * h->W16 : 0);
+  LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, march ? h->G * h->W16 : 0);
   return (size_t)L.total;
 }
 
@@ -1282,18 +1341,24 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   int rc = 0;
   if (h->d_grid) {  // re-load: release the previous terrain structures
     HIPCHK(hipDeviceSynchronize());
-    void *old[4] = {h->d_grid, h->d_mask2, h->d_mvtab, h->d_lostab};
+    void *old[5] = {h->d_grid, h->d_gridf, h->d_mask2, h->d_mvtab, h->d_lostab};
     for (void *p : old) {
       for (size_t i = 0; i < h->allocs.size(); i++)
         if (h->allocs[i] == p) { (void)hipFree(p); h->allocs.erase(h->allocs.begin() + i); break; }
     }
   }
   rc |= dalloc(h, &h->d_grid, (size_t)G * G);
+  rc |= dalloc(h, &h->d_gridf, (size_t)G * G);
   rc |= dalloc(h, &h->d_mask2, (size_t)G * h->W16);
   rc |= dalloc(h, &h->d_mvtab, (size_t)2 * G * G * MV_WORDS);
   rc |= dalloc(h, &h->d_lostab, (size_t)G * G * LOS_CELL_WORDS);
   if (rc) return rc;
   HIPCHK(hipMemcpy(h->d_grid, grid_host, (size_t)G * G, hipMemcpyHostToDevice));
+  {  // observation window values grid/255 (combatant.py:177), float64 quotient -> float32
+    std::vector<float> gf((size_t)G * G);
+    for (size_t i = 0; i < gf.size(); i++) gf[i] = (float)((double)grid_host[i] / 255.0);
+    HIPCHK(hipMemcpy(h->d_gridf, gf.data(), gf.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
   KParams &k = h->kp;
   k.G = G;
   k.W16 = h->W16;
@@ -1308,11 +1373,17 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   h->terrain = true;
-  // large dynamic LDS for the march variants
-  (void)hipFuncSetAttribute((const void *)step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void *)step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void *)observe_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void *)observe_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  // dynamic LDS above the 64 KiB default needs an explicit opt-in
+  for (int m = 0; m < 2; m++) {
+    size_t need = step_lds_bytes(h, m == 1) + 1024;
+    if (need > 64 * 1024) {
+      if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
+      const void *ks[2] = {m ? (const void *)step_kernel<true> : (const void *)step_kernel<false>,
+                           m ? (const void *)observe_kernel<true> : (const void *)observe_kernel<false>};
+      for (const void *k : ks) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+    }
+  }
+  (void)hipGetLastError();
   return 0;
 }
 
@@ -1370,6 +1441,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
     return fail(LNW_EINVAL, "integer actions go with DISCRETE mode and only with it");
   KParams k = h->kp;
   k.act_dtype = action_dtype;
+  if (const char *dbg = getenv("LNW_DEBUG_SKIP")) k.dbg_skip = atoi(dbg);
   KState s = make_state(h);
   bool march = k.los_mode == 1;
   size_t lds = step_lds_bytes(h, march);

@@ -34,8 +34,23 @@ def lib():
     return _abi.load()
 
 
+_KEEP = []
+
+
 def _dev(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    """Device copy that stays alive until the next test (a raw pointer taken from
+    a temporary would let the caching allocator hand its block to the next
+    argument before the kernel runs)."""
+    t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    _KEEP.append(t)
+    return t
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
 
 
 def _p(t):
