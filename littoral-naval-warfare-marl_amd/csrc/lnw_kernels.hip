@@ -38,7 +38,7 @@ struct LdsLayout {
   // persistent through phase O
   int pos_cur, pos_old, radar_cur, radar_old, tcnt, miss_cur, miss_old, type, alive0, obsd;
   // phase-S scratch (dead before phase O) ...
-  int pos_new, reward, observed, open, mkind, eng, bcnt, border;
+  int pos_new, reward, observed, open, mkind, eng, bcnt, border, steps, act0, act1, akind;
   // ... aliased by the phase-O row staging area
   int stage, mask, total;
 };
@@ -67,14 +67,20 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   const int scratch = o;
   L.stage = scratch;
   L.pos_new = o; o += A * PAD * 4;
+  L.steps = o; o += A * PAD * 4;
   o = (o + 7) & ~7;
-  L.reward = o; o += A * PAD * 8;
+  // the A* open lists (phase M) alias the rewards (first written in phase S)
+  L.reward = o;
+  L.open = o;
+  o += (A * PAD * 8 > OPEN_CAP * WAVE * 4) ? A * PAD * 8 : OPEN_CAP * WAVE * 4;
+  L.act0 = o; o += A * PAD * 8;
+  L.act1 = o; o += A * PAD * 8;
   L.observed = o; o += nmax * PAD * 4;
-  L.open = o; o += OPEN_CAP * WAVE * 4;
   L.mkind = o; o += A * PADB;
   L.eng = o; o += A * PADB;
   L.bcnt = o; o += nmax * PADB;
   L.border = o; o += nmax * PADB;
+  L.akind = o; o += A * PADB;
   int st_end = scratch + stage_bytes(A, nb, nr);
   if (st_end > o) o = st_end;
   o = (o + 15) & ~15;
@@ -85,9 +91,9 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
 
 struct Cols {
   uint32_t *pos_cur, *pos_old, *pos_new, *tcnt, *observed, *open;
-  int32_t *radar_cur, *radar_old;
-  double *reward;
-  uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border;
+  int32_t *radar_cur, *radar_old, *steps;
+  double *reward, *act0, *act1;
+  uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border, *akind;
   uint32_t *mask;
   float *stage;
 };
@@ -100,6 +106,10 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
   c.radar_cur = (int32_t *)(base + L.radar_cur);
   c.radar_old = (int32_t *)(base + L.radar_old);
   c.reward = (double *)(base + L.reward);
+  c.act0 = (double *)(base + L.act0);
+  c.act1 = (double *)(base + L.act1);
+  c.steps = (int32_t *)(base + L.steps);
+  c.akind = (uint8_t *)(base + L.akind);
   c.tcnt = (uint32_t *)(base + L.tcnt);
   c.observed = (uint32_t *)(base + L.observed);
   c.open = (uint32_t *)(base + L.open);
@@ -419,8 +429,8 @@ __device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int 
   Cols &c = X.c;
   const int lane = X.lane;
   size_t ai = (size_t)a * X.E + X.env;
-  int steps = S.steps[ai] + 1;
-  S.steps[ai] = steps;
+  int steps = COLW(c.steps, a) + 1;
+  COLW(c.steps, a) = steps;
   int tl_n = (int)COLW(c.tcnt, a);
   double r = 0.0;
   if (tl_n > 0) r += (double)(tl_n * 3);
@@ -547,6 +557,10 @@ __device__ inline Rng make_rng(const KParams &P, const KState &S, int env) {
 // wave then copies each side's block ([envs][n][D], contiguous in the output)
 // out with consecutive lanes on consecutive floats (256-B coalesced stores).
 // ---------------------------------------------------------------------------
+// Builds one observation row of D floats into an LDS row (stride D+1: odd, so
+// a ds_write_b32 across lanes is conflict-free). The terrain window comes from
+// the per-cell window table (Combatant 49 floats padded to 52, LandingShip 25
+// padded to 28): 13 / 7 independent float4 loads issued together.
 __device__ void build_row(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
                           int el, int k, float *row, bool only_observed) {
   const int side = k >= P.nb;
@@ -565,26 +579,27 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
   int idx;
   if (tk == T_LS) {
     // asymmetric 5x5 window rows/cols pos-1..pos+3 (landingship.py:178-188)
+    const float4 *w = (const float4 *)(S.winf + (size_t)G * G * 52 + (size_t)(px * G + py) * 28);
+    float4 v[7];
 #pragma unroll
-    for (int i = 0; i < 5; i++) {
-      const int x = px - 1 + i;
+    for (int q = 0; q < 7; q++) v[q] = w[q];
 #pragma unroll
-      for (int j = 0; j < 5; j++) {
-        const int y = py - 1 + j;
-        row[i * 5 + j] = (0 <= x && x < 100 && 0 <= y && y < 100) ? S.gridf[x * G + y] : 0.0f;
-      }
+    for (int q = 0; q < 6; q++) {
+      row[4 * q] = v[q].x; row[4 * q + 1] = v[q].y; row[4 * q + 2] = v[q].z; row[4 * q + 3] = v[q].w;
     }
+    row[24] = v[6].x;
     idx = 25;
   } else {
+    // 7x7 window around the ship (combatant.py:174-181)
+    const float4 *w = (const float4 *)(S.winf + (size_t)(px * G + py) * 52);
+    float4 v[13];
 #pragma unroll
-    for (int i = 0; i < 7; i++) {
-      const int x = px - 3 + i;
+    for (int q = 0; q < 13; q++) v[q] = w[q];
 #pragma unroll
-      for (int j = 0; j < 7; j++) {
-        const int y = py - 3 + j;
-        row[i * 7 + j] = (0 <= x && x < 100 && 0 <= y && y < 100) ? S.gridf[x * G + y] : 0.0f;
-      }
+    for (int q = 0; q < 12; q++) {
+      row[4 * q] = v[q].x; row[4 * q + 1] = v[q].y; row[4 * q + 2] = v[q].z; row[4 * q + 3] = v[q].w;
     }
+    row[48] = v[12].x;
     idx = 49;
   }
   row[idx++] = (float)((double)px / (double)G);
@@ -614,17 +629,30 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
   for (; idx < D; idx++) row[idx] = 0.0f;
 }
 
+// Copy one side's block [ne envs][ns rows][D] (contiguous in the output, a
+// multiple of 4 floats and 16-B aligned since D = 4*ns + 52) with each lane
+// storing 4 consecutive floats: 1 KiB per wave store instruction.
 __device__ inline void copy_side(const float *stage, float *out, int ns, int ne, long long genv0) {
   if (!out) return;
   const int lane = threadIdx.x;
   const int D = 4 * ns + 52;
   const int n = ne * ns * D;
-  float *base = out + (size_t)genv0 * ns * D;
-  int row = lane / D, col = lane - (lane / D) * D;
-  for (int i = lane; i < n; i += WAVE) {
-    base[i] = stage[row * (D + 1) + col];
-    col += WAVE;
-    while (col >= D) { col -= D; row++; }
+  float4 *base = (float4 *)(out + (size_t)genv0 * ns * D);
+  const int i0 = 4 * lane;
+  int r = i0 / D, col = i0 - r * D;
+  for (int i = i0; i < n; i += 4 * WAVE) {
+    float4 v;
+    int rr = r, cc = col;
+    v.x = stage[rr * (D + 1) + cc];
+    if (++cc == D) { cc = 0; rr++; }
+    v.y = stage[rr * (D + 1) + cc];
+    if (++cc == D) { cc = 0; rr++; }
+    v.z = stage[rr * (D + 1) + cc];
+    if (++cc == D) { cc = 0; rr++; }
+    v.w = stage[rr * (D + 1) + cc];
+    base[i >> 2] = v;
+    col += 4 * WAVE;
+    while (col >= D) { col -= D; r++; }
   }
 }
 
@@ -672,6 +700,7 @@ __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, in
       COLB(c.type, a) = S.type[ai];
       COLB(c.alive0, a) = S.alive[ai];
       COLW(c.tcnt, a) = S.tl_cnt[ai];
+      COLW(c.steps, a) = S.steps[ai];
       COLB(c.eng, a) = 0;
       COLB(c.mkind, a) = S.mkind[ai];
       COLB(c.obsd, a) = 0;
@@ -699,21 +728,20 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   const bool valid = env < E;
   const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
   const int A = P.A, nb = P.nb, nr = P.nr;
-  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, MARCH ? P.G * P.W16 : 0);
+  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
 
-  const uint32_t *mask = S.mask2;
-  if (MARCH) {
-    for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
-    mask = c.mask;
-  }
+  for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
+  const uint32_t *mask = c.mask;
   load_state(P, S, c, lane, env, valid);
   double duct = valid ? S.duct[env] : 1.0;
   duct_col[lane] = duct;
   __syncthreads();
 
   // ---- phase M: movement feasibility for every agent of this env --------
+  // M1: load each action row once (a0/a1 kept in LDS for phase S) and compute
+  //     the move target; M2: feasibility lookups (independent across agents).
   const int dt = P.act_dtype;
   if (valid && !(P.dbg_skip & 4)) {
     for (int a = 0; a < A; a++) {
@@ -722,41 +750,54 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
       int sx = pos_x(p), sy = pos_y(p);
       int t = COLB(c.type, a);
       size_t row = ((size_t)env * A + a) * 4;
-      bool feas = false;
-      int tx = sx, ty = sy;
+      uint32_t target = p;  // no candidate
       if (dt == LNW_ACT_I32) {
-        int v = ((const int32_t *)actions)[row + 2];
-        int x = floordiv7(v), y = pymod7(v);
-        if (0 <= sx - 3 + x && sx - 3 + x < P.G && 0 <= sy - 3 + y && sy - 3 + y < P.G) {
-          tx = sx - 3 + x;
-          ty = sy - 3 + y;
-          feas = check_path_h(P, S, t, sx, sy, tx, ty, c.open + lane, WAVE);
-        }
+        int4 v = *(const int4 *)((const int32_t *)actions + row);
+        COLW(c.act0, a) = (double)v.x;
+        COLW(c.act1, a) = (double)v.y;
+        COLB(c.akind, a) = K_PYINT;
+        int x = floordiv7(v.z), y = pymod7(v.z);
+        if (0 <= sx - 3 + x && sx - 3 + x < P.G && 0 <= sy - 3 + y && sy - 3 + y < P.G)
+          target = pack_pos(sx - 3 + x, sy - 3 + y) | 0x40000000u;
       } else {
         double a2, a3;
         int kind;
         if (dt == LNW_ACT_F32) {
-          const float *fa = (const float *)actions;
-          a2 = fa[row + 2];
-          a3 = fa[row + 3];
+          float4 v = *(const float4 *)((const float *)actions + row);
+          COLW(c.act0, a) = v.x;
+          COLW(c.act1, a) = v.y;
+          a2 = v.z;
+          a3 = v.w;
           kind = K_F32;
         } else {
-          const double *da = (const double *)actions;
-          a2 = da[row + 2];
-          a3 = da[row + 3];
+          const double2 *da = (const double2 *)((const double *)actions + row);
+          double2 v01 = da[0], v23 = da[1];
+          COLW(c.act0, a) = v01.x;
+          COLW(c.act1, a) = v01.y;
+          a2 = v23.x;
+          a3 = v23.y;
           kind = row_kind ? row_kind[(size_t)env * A + a] : K_F64;
         }
+        COLB(c.akind, a) = (uint8_t)kind;
         int nx, ny;
         bool ok = move_target_dev(sx, sy, ship_speed(t), a2, a3, kind, nx, ny);
         if (!ok) {
           S.err[env] |= LNW_ERRF_NAN_ROUND;
-        } else if (can_move_to_h(P, S, nx, ny)) {
-          feas = check_path_h(P, S, t, sx, sy, nx, ny, c.open + lane, WAVE);
-          tx = nx;
-          ty = ny;
+        } else if (0 <= nx && nx < 100 && 0 <= ny && ny < 100 &&
+                   !(cell_bits(mask, P.W16, nx, ny) & 1u)) {  // can_move_to (combatant.py:482-489)
+          target = pack_pos(nx, ny) | 0x40000000u;
         }
       }
-      COLW(c.pos_new, a) = feas ? (pack_pos(tx, ty) | 0x80000000u) : p;
+      COLW(c.pos_new, a) = target;
+    }
+    for (int a = 0; a < A; a++) {
+      uint32_t tg = COLW(c.pos_new, a);
+      if (!(tg & 0x40000000u)) continue;
+      uint32_t p = COLW(c.pos_old, a);
+      const uint32_t t2 = tg & 0x3fffffffu;
+      bool feas = check_path_h(P, S, COLB(c.type, a), pos_x(p), pos_y(p), pos_x(t2), pos_y(t2),
+                               c.open + lane, WAVE);
+      COLW(c.pos_new, a) = feas ? ((tg & 0x3fffffffu) | 0x80000000u) : p;
     }
   }
 
@@ -766,6 +807,9 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   if (valid && !(P.dbg_skip & 2)) {
     Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E};
     Neut N{{0, 0}, {0u, 0u}};
+    int ev[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) ev[q] = S.envi[q * E + env];
     int hits[2] = {0, 0};
     double bsx = 0, bsy = 0, rsx = 0, rsy = 0;
     int nbp = 0, nrp = 0;
@@ -779,19 +823,8 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
         rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
       }
       size_t row = ((size_t)env * A + a) * 4;
-      double a0, a1;
-      int kind;
-      if (dt == LNW_ACT_F32) {
-        const float *fa = (const float *)actions;
-        a0 = fa[row]; a1 = fa[row + 1]; kind = K_F32;
-      } else if (dt == LNW_ACT_F64) {
-        const double *da = (const double *)actions;
-        a0 = da[row]; a1 = da[row + 1];
-        kind = row_kind ? row_kind[(size_t)env * A + a] : K_F64;
-      } else {
-        const int32_t *ia = (const int32_t *)actions;
-        a0 = ia[row]; a1 = ia[row + 1]; kind = K_PYINT;
-      }
+      double a0 = COLW(c.act0, a), a1 = COLW(c.act1, a);
+      int kind = COLB(c.akind, a);
       // untrained red: random salvo (game.py:375-379), written back in place
       if (side && !P.trained_red) {
         if (X.rng.uniform() < P.red_aggression) {
@@ -822,7 +855,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
           if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
         }
       }
-      S.envi[(5 + side) * E + env] += destroyed;
+      if (side) ev[6] += destroyed; else ev[5] += destroyed;
       if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
       else {
         double rr = rint(a0);
@@ -842,10 +875,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
       hits[side] += destroyed;
     }
     // ---- tail (game.py:409-520) -------------------------------------------
-    int nbl = S.envi[0 * E + env] - N.cnt[0];
-    int nrl = S.envi[1 * E + env] - N.cnt[1];
-    S.envi[0 * E + env] = nbl;
-    S.envi[1 * E + env] = nrl;
+    int nbl = ev[0] - N.cnt[0];
+    int nrl = ev[1] - N.cnt[1];
+    ev[0] = nbl;
+    ev[1] = nrl;
     bool no_blue = nbl == 0, no_red = nrl == 0;
     for (int a = 0; a < A; a++) {
       if (!COLB(c.alive0, a)) continue;
@@ -864,7 +897,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
         if (a < nb) { if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a); }
         else COLW(c.reward, a) += 100.0;
       }
-      S.envi[4 * E + env] += 1;
+      ev[4] += 1;
     }
     if (no_red && !no_blue) {
       done = 0;
@@ -872,7 +905,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
         if (a < nb) COLW(c.reward, a) += 100.0;
         else if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
       }
-      S.envi[3 * E + env] += 1;
+      ev[3] += 1;
     }
     if (no_blue && no_red) {
       done = 0;
@@ -887,7 +920,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
           if (a < nb) COLW(c.reward, a) += 100.0;
           else COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
         }
-        S.envi[3 * E + env] += 1;
+        ev[3] += 1;
       } else {
         for (int l = nb; l < A; l++) {
           if (!(COLB(c.alive0, l) && COLB(c.type, l) == T_LS)) continue;
@@ -898,13 +931,13 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
               if (a < nb) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
               else COLW(c.reward, a) += 100.0;
             }
-            S.envi[3 * E + env] += 1;
+            ev[3] += 1;
           }
         }
       }
     }
-    int steps_env = S.envi[2 * E + env] + 1;
-    S.envi[2 * E + env] = steps_env;
+    int steps_env = ev[2] + 1;
+    ev[2] = steps_env;
     if (nbp > 0 && nrp > 0) {
       double bx = bsx / nbp, by = bsy / nbp, rx = rsx / nrp, ry = rsy / nrp;
       cog = (float)sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
@@ -928,7 +961,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
       S.mkind[ai] = COLB(c.mkind, a);
       S.alive[ai] = COLB(c.alive0, a) && !killed;
       S.tl_cnt[ai] = (uint16_t)COLW(c.tcnt, a);
+      S.steps[ai] = COLW(c.steps, a);
     }
+#pragma unroll
+    for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
     if (do_reset) reset_env_dev(P, S, env, X.rng);
     S.rng[env] = X.rng.ctr;
     if (X.rng.err) S.err[env] |= X.rng.err;
@@ -952,14 +988,11 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   const bool valid = env < E;
   const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
   const int A = P.A, nb = P.nb;
-  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, MARCH ? P.G * P.W16 : 0);
+  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
-  const uint32_t *mask = S.mask2;
-  if (MARCH) {
-    for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
-    mask = c.mask;
-  }
+  for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
+  const uint32_t *mask = c.mask;
   load_state(P, S, c, lane, env, valid);
   double duct = valid ? S.duct[env] : 1.0;
   duct_col[lane] = duct;
@@ -1201,7 +1234,7 @@ struct lnw_handle {
   bool terrain = false;
   // device buffers
   uint8_t *d_grid = nullptr;
-  float *d_gridf = nullptr;
+  float *d_gridf = nullptr, *d_winf = nullptr;
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -1236,7 +1269,7 @@ KState make_state(lnw_handle *h) {
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
   s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
-  s.grid = h->d_grid; s.gridf = h->d_gridf; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
   s.sp_pos_env = nullptr;
@@ -1245,7 +1278,7 @@ KState make_state(lnw_handle *h) {
 }
 
 size_t step_lds_bytes(const lnw_handle *h, bool march) {
-  LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, march ? h->G * h->W16 : 0);
+  LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16);
   return (size_t)L.total;
 }
 
@@ -1341,7 +1374,7 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   int rc = 0;
   if (h->d_grid) {  // re-load: release the previous terrain structures
     HIPCHK(hipDeviceSynchronize());
-    void *old[5] = {h->d_grid, h->d_gridf, h->d_mask2, h->d_mvtab, h->d_lostab};
+    void *old[6] = {h->d_grid, h->d_gridf, h->d_winf, h->d_mask2, h->d_mvtab, h->d_lostab};
     for (void *p : old) {
       for (size_t i = 0; i < h->allocs.size(); i++)
         if (h->allocs[i] == p) { (void)hipFree(p); h->allocs.erase(h->allocs.begin() + i); break; }
@@ -1349,6 +1382,7 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   }
   rc |= dalloc(h, &h->d_grid, (size_t)G * G);
   rc |= dalloc(h, &h->d_gridf, (size_t)G * G);
+  rc |= dalloc(h, &h->d_winf, (size_t)G * G * (52 + 28));
   rc |= dalloc(h, &h->d_mask2, (size_t)G * h->W16);
   rc |= dalloc(h, &h->d_mvtab, (size_t)2 * G * G * MV_WORDS);
   rc |= dalloc(h, &h->d_lostab, (size_t)G * G * LOS_CELL_WORDS);
@@ -1358,6 +1392,23 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     std::vector<float> gf((size_t)G * G);
     for (size_t i = 0; i < gf.size(); i++) gf[i] = (float)((double)grid_host[i] / 255.0);
     HIPCHK(hipMemcpy(h->d_gridf, gf.data(), gf.size() * sizeof(float), hipMemcpyHostToDevice));
+    // per-cell observation windows: Combatant 7x7 around the ship (49 floats,
+    // padded to 52), LandingShip 5x5 rows/cols pos-1..pos+3 (25, padded to 28);
+    // cells outside the hard-coded 0..99 are 0 (combatant.py:176)
+    std::vector<float> wf((size_t)G * G * (52 + 28), 0.0f);
+    auto cellv = [&](int x, int y) {
+      return (0 <= x && x < 100 && 0 <= y && y < 100 && x < G && y < G) ? gf[(size_t)x * G + y] : 0.0f;
+    };
+    for (int x = 0; x < G; x++)
+      for (int y = 0; y < G; y++) {
+        float *w7 = &wf[((size_t)x * G + y) * 52];
+        for (int i = 0; i < 7; i++)
+          for (int j = 0; j < 7; j++) w7[i * 7 + j] = cellv(x - 3 + i, y - 3 + j);
+        float *w5 = &wf[(size_t)G * G * 52 + ((size_t)x * G + y) * 28];
+        for (int i = 0; i < 5; i++)
+          for (int j = 0; j < 5; j++) w5[i * 5 + j] = cellv(x - 1 + i, y - 1 + j);
+      }
+    HIPCHK(hipMemcpy(h->d_winf, wf.data(), wf.size() * sizeof(float), hipMemcpyHostToDevice));
   }
   KParams &k = h->kp;
   k.G = G;
