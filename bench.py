@@ -92,8 +92,8 @@ def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmu
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
-    if world > 1:
-        torch.distributed.barrier()
+    from lnw import dist
+    dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(steps):
@@ -101,8 +101,7 @@ def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmu
         g.step(acts[warmup + s])
         ev[s][1].record()
     torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kms = [a.elapsed_time(b) for a, b in ev]
@@ -147,19 +146,14 @@ def cpu_baseline(seconds):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from lnw import dist
+    world, rank, local = dist.world()
     torch.cuda.set_device(local)
-    if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist.init("nccl")
     E = args.envs
     elapsed, kms_mean, kms_med, err, episodes = run_workload(
         E, rank, world, args, args.spawns, args.los_mode, args.move_mode, args.steps, args.warmup)
-    t = torch.tensor([elapsed, kms_mean], dtype=torch.float64, device="cuda")
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed, kms_mean = float(t[0]), float(t[1])
+    elapsed, kms_mean = dist.reduce_max([elapsed, kms_mean])
     value = world * E * args.steps / elapsed
     nb = nr = 4
     B = algorithmic_bytes(nb, nr)
@@ -174,7 +168,7 @@ def main():
         except Exception:
             traffic = None
     secondary = {}
-    if args.secondary and rank == 0:
+    if args.secondary and world == 1:
         for name, sp, lm, mm in (("melee", "melee", 0, 0), ("reference_march_astar", "reference", 1, 1),
                                  ("melee_march_astar", "melee", 1, 1)):
             el, km, _, er, _ = run_workload(E, rank, 1, args, sp, lm, mm, args.steps, args.warmup)
@@ -216,8 +210,7 @@ def main():
         if secondary:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    dist.finalize()
 
 
 if __name__ == "__main__":

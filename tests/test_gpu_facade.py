@@ -1,0 +1,85 @@
+"""The reference-compatible Game facade (lnw.game) used the way ppo.py / main.py
+use game.Game: per-ship get_obs() then step(list of action rows), checked
+step by step against the CPU oracle stepping the same environment."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_for(game):
+    sc = game.scenario
+    o = _oracle.OracleEnv(np.asarray(game.grid, np.uint8), len(game.blue_ships),
+                          len(game.red_ships), discrete=sc.discrete, landing_ops=sc.landing_ops,
+                          aggressive=sc.tactics == "aggressive", side_blue=sc.side == "blue",
+                          trained_red=sc.trained_red, red_aggression=sc.red_aggression)
+    return o
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_facade_rollout_matches_oracle(seed, tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)  # no config.json / PNG here: defaults + packaged grid
+    from lnw.game import Game, ShipSpec
+    random.seed(seed)
+    np.random.seed(seed)
+    g = Game()
+    g.scenario.landing_ops = False
+    g.scenario.n_red_landingship = 0
+    blue = [ShipSpec("blue", "small", p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
+    red = [ShipSpec("red", "large", p) for p in [(58, 55), (60, 60), (62, 52), (57, 64)]]
+    state = random.getstate()
+    g.reset(4, 4, blue_ships=blue, red_ships=red)
+    # replicate the facade's seeds: it draws its Philox seed from `random` at reset
+    random.setstate(state)
+    seed63 = random.getrandbits(63)
+    o = _oracle_for(g)
+    o.set_philox(seed63, 0)
+    o.reset([0] * 4 + [1] * 4, [s.position for s in blue + red])
+    o.set_ducting(g.ducting_factor)
+    rng = np.random.default_rng(seed)
+    for step in range(25):
+        for i, ship in enumerate(g.blue_ships):
+            if ship is not None:
+                got = ship.get_obs()
+                ref = o.observe(i)
+                assert np.array_equal(got.astype(np.float32), ref.astype(np.float32)), (step, i)
+                assert ship.target_list == o.tlist(i)
+        acts = [rng.random(4).astype(np.float32) for _ in range(8)]
+        obs, rew, done, cog = g.step(acts)
+        r = o.step(np.array(acts, np.float64), np.full(8, _oracle.K_F32, np.int32))
+        assert np.array_equal(obs[0].astype(np.float32), r["obs_blue"].astype(np.float32)), step
+        np.testing.assert_allclose(rew, r["rew_blue"], rtol=1e-6, atol=1e-5)
+        assert done == r["done"]
+        if cog is None:
+            assert np.isnan(r["cog"])
+        else:
+            assert abs(cog - r["cog"]) < 1e-4
+        st = o.agents()
+        for i, ship in enumerate(g.blue_ships + g.red_ships):
+            assert (ship is None) == (st["alive"][i] == 0)
+            if ship is not None:
+                assert ship.position == tuple(st["pos"][i])
+                assert ship.missiles == st["missiles"][i]
+        if done == 0:
+            break
+    g.close()
+
+
+def test_facade_default_reset_and_shapes(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    from lnw.game import Game
+    g = Game()
+    g.reset(3, 2)  # shipped config: 3 blue, 2 red + 1 landing ship (random spawn)
+    assert len(g.blue_ships) == 3 and len(g.red_ships) == 3
+    assert g.red_ships[-1].ship_type == "ls"
+    assert g.observation_space == 3 * 4 + 52 and g.red_observation_space == 3 * 4 + 52
+    ls = g.red_ships[-1]
+    assert ls.position[0] in (98, 99) and 48 <= ls.position[1] <= 56
+    obs, rew, done, cog = g.step([np.zeros(4, np.float32)] * 6)
+    assert obs.shape == (1, 3, g.observation_space) and len(rew) == 3
+    g.close()

@@ -324,3 +324,30 @@ def test_episode_gpu_tape_march_astar(name, grids):
     if not os.path.exists(os.path.join(GOLDEN, name)):
         pytest.skip("fixture absent")
     _cmp_episode(name, grids, los_mode=1, move_mode=1)
+
+
+def test_shard_invariance(grids):
+    """Env sharding: two handles holding global envs [0,32) and [32,64) produce
+    exactly the trajectories of one handle holding [0,64) (RNG keyed by global
+    env id; melee box spawns drawn per global id too)."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40)
+    box = ((40, 40), (57, 65))
+    pos = [(6, 61), (10, 81), (8, 70), (11, 58), (98, 48), (98, 52), (98, 56), (96, 52)]
+    full = BatchedGame(64, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=5)
+    parts = [BatchedGame(32, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=5,
+                         env_id_base=b) for b in (0, 32)]
+    for g in [full] + parts:
+        g.reset(positions=pos, box=box)
+    rng = np.random.default_rng(0)
+    for s in range(60):
+        act = torch.from_numpy(rng.random((64, 8, 4)).astype(np.float32)).cuda()
+        of = {k: v.cpu().numpy().copy() for k, v in full.step(act.clone()).items()}
+        op = [{k: v.cpu().numpy().copy() for k, v in g.step(act[32 * i:32 * (i + 1)].clone()).items()}
+              for i, g in enumerate(parts)]
+        for k in of:
+            merged = np.concatenate([op[0][k], op[1][k]])
+            assert np.array_equal(of[k], merged, equal_nan=True), (s, k)
+    for g in [full] + parts:
+        g.close()
