@@ -28,8 +28,12 @@ using namespace lnw;
 
 namespace {
 
-constexpr int PAD = WAVE + 1;   // padded LDS column stride (words) -> no bank conflicts
-constexpr int PADB = WAVE + 4;  // byte-array stride
+#ifndef LNW_EPW
+#define LNW_EPW 64
+#endif
+constexpr int EPW = LNW_EPW;    // environments per wavefront (= per workgroup)
+constexpr int PAD = EPW + 1;    // padded LDS column stride (words) -> no bank conflicts
+constexpr int PADB = EPW + 4;   // byte-array stride
 
 // ---------------------------------------------------------------------------
 // per-wave LDS carve-up for the step/observe kernels
@@ -43,14 +47,26 @@ struct LdsLayout {
   int stage, mask, total;
 };
 
-// Row staging for phase O: up to 64 observation rows of D+1 floats (odd stride
-// -> conflict-free ds_write_b32 across lanes).
-__host__ __device__ inline int stage_bytes(int A, int nb, int nr) {
-  int epg = WAVE / A;
-  return epg * (nb * (4 * nb + 53) + nr * (4 * nr + 53)) * 4;
+// Row staging for phase O: up to 64 observation rows. The row stride S (floats)
+// is a multiple of 4 with S/4 odd: rows are 16-B aligned so the copy-out reads
+// float4s (ds_read_b128, conflict-free), and row starts spread over 8 banks
+// (ds_write_b32 from lanes on different rows is at most 2-way).
+__host__ __device__ inline int stage_stride(int ns) {
+  int D = 4 * ns + 52;
+  return ((D / 4) & 1) ? D : D + 4;
+}
+// Phase-O LDS: staged rows (one pass = the rows of WAVE/A envs) | x/G LUT.
+__host__ __device__ inline int envs_per_pass(int A) { return WAVE / A; }
+__host__ __device__ inline int stage_rows_bytes(int A, int nb, int nr) {
+  int epg = envs_per_pass(A);
+  return epg * (nb * stage_stride(nb) + nr * stage_stride(nr)) * 4;
+}
+__host__ __device__ inline int stage_bytes(int A, int nb, int nr, int G) {
+  return stage_rows_bytes(A, nb, nr) + ((G + 3) & ~3) * 4;
 }
 
-__host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax, int mask_words) {
+__host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax, int mask_words,
+                                                int G) {
   LdsLayout L;
   int o = 0;
   L.pos_cur = o; o += A * PAD * 4;
@@ -81,7 +97,7 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   L.bcnt = o; o += nmax * PADB;
   L.border = o; o += nmax * PADB;
   L.akind = o; o += A * PADB;
-  int st_end = scratch + stage_bytes(A, nb, nr);
+  int st_end = scratch + stage_bytes(A, nb, nr, G);
   if (st_end > o) o = st_end;
   o = (o + 15) & ~15;
   L.mask = o; o += mask_words * 4;
@@ -140,7 +156,18 @@ struct Ctx {
   Rng rng;
   const uint32_t *mask;  // LDS (march mode) or global
   long long E;
+  int r2max;             // max over ship-type pairs of radar^2, EW^2 and 16 (d < 4)
 };
+
+__device__ inline int max_range2(const KParams &P, double duct) {
+  int m = 16;
+  for (int ti = 0; ti < 3; ti++)
+    for (int tj = 0; tj < 3; tj++) {
+      int r = radar_r(P, duct, ti, tj), e = ew_r(P, duct, ti, tj);
+      m = max(m, max(r * r, e * e));
+    }
+  return m;
+}
 
 __device__ inline int floordiv7(int v) { int q = v / 7; if ((v % 7 != 0) && (v < 0)) q--; return q; }
 __device__ inline int pymod7(int v) { int m = v % 7; if (m < 0) m += 7; return m; }
@@ -214,6 +241,7 @@ __device__ void get_obs_dev(Ctx &X, int me) {
       int tj = COLB(c.type, j);
       int dx = xj - xi, dy = yj - yi;
       int d2 = dx * dx + dy * dy;
+      if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
       int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
       bool rad_ok = myradar == 1 && d2 < rr * rr;
       bool close = d2 < 16;
@@ -562,7 +590,7 @@ __device__ inline Rng make_rng(const KParams &P, const KState &S, int env) {
 // the per-cell window table (Combatant 49 floats padded to 52, LandingShip 25
 // padded to 28): 13 / 7 independent float4 loads issued together.
 __device__ void build_row(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
-                          int el, int k, float *row, bool only_observed) {
+                          int el, int k, float *row, const float *xg, bool only_observed) {
   const int side = k >= P.nb;
   const int own0 = side ? P.nb : 0;
   const int ns = side ? P.nr : P.nb;
@@ -583,10 +611,9 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
     float4 v[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) v[q] = w[q];
+    float4 *r4 = (float4 *)row;
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-      row[4 * q] = v[q].x; row[4 * q + 1] = v[q].y; row[4 * q + 2] = v[q].z; row[4 * q + 3] = v[q].w;
-    }
+    for (int q = 0; q < 6; q++) r4[q] = v[q];
     row[24] = v[6].x;
     idx = 25;
   } else {
@@ -595,17 +622,17 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
     float4 v[13];
 #pragma unroll
     for (int q = 0; q < 13; q++) v[q] = w[q];
+    float4 *r4 = (float4 *)row;
 #pragma unroll
-    for (int q = 0; q < 12; q++) {
-      row[4 * q] = v[q].x; row[4 * q + 1] = v[q].y; row[4 * q + 2] = v[q].z; row[4 * q + 3] = v[q].w;
-    }
+    for (int q = 0; q < 12; q++) r4[q] = v[q];
     row[48] = v[12].x;
     idx = 49;
   }
-  row[idx++] = (float)((double)px / (double)G);
-  row[idx++] = (float)((double)py / (double)G);
+  // missiles/4 and missiles/8 are exact in float32
+  row[idx++] = xg[px];
+  row[idx++] = xg[py];
   row[idx++] = (float)c.radar_cur[k * PAD + el];
-  row[idx++] = (float)((double)c.miss_cur[k * PADB + el] / miss_norm(tk));
+  row[idx++] = (float)c.miss_cur[k * PADB + el] * (tk == T_SMALL ? 0.25f : 0.125f);
   for (int il = 0; il < ns; il++) {
     if (il == kl) continue;
     const int i = own0 + il;
@@ -613,11 +640,11 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
       // own ships that acted before k this step show their new state
       const bool nw = il < kl;
       const uint32_t q = nw ? c.pos_cur[i * PAD + el] : c.pos_old[i * PAD + el];
-      row[idx] = (float)((double)pos_x(q) / (double)G);
-      row[idx + 1] = (float)((double)pos_y(q) / (double)G);
+      row[idx] = xg[pos_x(q)];
+      row[idx + 1] = xg[pos_y(q)];
       row[idx + 2] = (float)(nw ? c.radar_cur[i * PAD + el] : c.radar_old[i * PAD + el]);
       const int m = nw ? c.miss_cur[i * PADB + el] : c.miss_old[i * PADB + el];
-      row[idx + 3] = (float)((double)m / miss_norm(c.type[i * PADB + el]));
+      row[idx + 3] = (float)m * (c.type[i * PADB + el] == T_SMALL ? 0.25f : 0.125f);
     } else {
       row[idx] = row[idx + 1] = row[idx + 2] = row[idx + 3] = 0.0f;
     }
@@ -631,50 +658,56 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
 
 // Copy one side's block [ne envs][ns rows][D] (contiguous in the output, a
 // multiple of 4 floats and 16-B aligned since D = 4*ns + 52) with each lane
-// storing 4 consecutive floats: 1 KiB per wave store instruction.
+// moving 4 consecutive floats: ds_read_b128 from the staged row, dwordx4 store
+// (1 KiB per wave store instruction).
 __device__ inline void copy_side(const float *stage, float *out, int ns, int ne, long long genv0) {
   if (!out) return;
   const int lane = threadIdx.x;
   const int D = 4 * ns + 52;
-  const int n = ne * ns * D;
+  const int S4 = stage_stride(ns) >> 2;
+  const int D4 = D >> 2;
+  const int n4 = ne * ns * D4;
+  const float4 *st4 = (const float4 *)stage;
   float4 *base = (float4 *)(out + (size_t)genv0 * ns * D);
-  const int i0 = 4 * lane;
-  int r = i0 / D, col = i0 - r * D;
-  for (int i = i0; i < n; i += 4 * WAVE) {
-    float4 v;
-    int rr = r, cc = col;
-    v.x = stage[rr * (D + 1) + cc];
-    if (++cc == D) { cc = 0; rr++; }
-    v.y = stage[rr * (D + 1) + cc];
-    if (++cc == D) { cc = 0; rr++; }
-    v.z = stage[rr * (D + 1) + cc];
-    if (++cc == D) { cc = 0; rr++; }
-    v.w = stage[rr * (D + 1) + cc];
-    base[i >> 2] = v;
-    col += 4 * WAVE;
-    while (col >= D) { col -= D; r++; }
+  int r = lane / D4, c4 = lane - r * D4;
+  for (int i = lane; i < n4; i += WAVE) {
+    base[i] = st4[r * S4 + c4];
+    c4 += WAVE;
+    while (c4 >= D4) { c4 -= D4; r++; }
   }
 }
+
+// The workgroup is a single wavefront: LDS traffic between its lanes only needs
+// the wave's LDS operations to have completed (DS ops of one wave execute in
+// order), not a workgroup barrier, which would also drain every outstanding
+// global store (s_waitcnt vmcnt(0)) each group.
+__device__ inline void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __device__ void write_obs(const KParams &P, const KState &S, Cols &c, const double *duct_col,
                           float *obs_b, float *obs_r, int env0, int nenv, bool only_observed) {
   const int lane = threadIdx.x;
   const int A = P.A, nb = P.nb, nr = P.nr;
-  const int epg = WAVE / A;
+  const int epg = envs_per_pass(A);
   const int my_e = lane / A, my_k = lane - (lane / A) * A;
   const int side = my_k >= nb;
   const int kl = side ? my_k - nb : my_k;
   const int ns = side ? nr : nb;
   float *stage_b = c.stage;
-  float *stage_r = c.stage + epg * nb * (4 * nb + 53);
-  float *row = (side ? stage_r : stage_b) + (my_e * ns + kl) * (4 * ns + 53);
+  float *stage_r = c.stage + epg * nb * stage_stride(nb);
+  float *row = (side ? stage_r : stage_b) + (my_e * ns + kl) * stage_stride(ns);
+  float *xg = stage_r + epg * nr * stage_stride(nr);  // x/G (float32 of the f64 quotient)
+  for (int x = lane; x < P.G; x += WAVE) xg[x] = (float)((double)x / (double)P.G);
+  wave_lds_sync();
   for (int g0 = 0; g0 < nenv; g0 += epg) {
     const int ne = (nenv - g0) < epg ? (nenv - g0) : epg;
-    if (my_e < ne) build_row(P, S, c, duct_col, g0 + my_e, my_k, row, only_observed);
-    __syncthreads();
-    copy_side(stage_b, obs_b, nb, ne, env0 + g0);
-    copy_side(stage_r, obs_r, nr, ne, env0 + g0);
-    __syncthreads();
+    if (my_e < ne && !(P.dbg_skip & 8))
+      build_row(P, S, c, duct_col, g0 + my_e, my_k, row, xg, only_observed);
+    wave_lds_sync();
+    if (!(P.dbg_skip & 16)) {
+      copy_side(stage_b, obs_b, nb, ne, env0 + g0);
+      copy_side(stage_r, obs_r, nr, ne, env0 + g0);
+    }
+    wave_lds_sync();
   }
 }
 
@@ -704,7 +737,7 @@ __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, in
       COLB(c.eng, a) = 0;
       COLB(c.mkind, a) = S.mkind[ai];
       COLB(c.obsd, a) = 0;
-    } else {
+    } else if (lane < EPW) {
       COLB(c.alive0, a) = 0;
       COLB(c.type, a) = 0;
     }
@@ -722,13 +755,13 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
                                                   float *obs_r, float *rew_b, float *rew_r,
                                                   int32_t *done_out, float *cog_out) {
   const int lane = threadIdx.x;
-  const int env0 = blockIdx.x * WAVE;
+  const int env0 = blockIdx.x * EPW;
   const int env = env0 + lane;
   const long long E = P.E;
-  const bool valid = env < E;
-  const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
+  const bool valid = lane < EPW && env < E;
+  const int nenv = (E - env0) < EPW ? (int)(E - env0) : EPW;
   const int A = P.A, nb = P.nb, nr = P.nr;
-  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16);
+  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
 
@@ -805,7 +838,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   int done = 1;
   float cog = NAN;
   if (valid && !(P.dbg_skip & 2)) {
-    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E};
+    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E, max_range2(P, duct)};
     Neut N{{0, 0}, {0u, 0u}};
     int ev[8];
 #pragma unroll
@@ -982,13 +1015,13 @@ template <bool MARCH>
 __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
                                                      float *obs_r) {
   const int lane = threadIdx.x;
-  const int env0 = blockIdx.x * WAVE;
+  const int env0 = blockIdx.x * EPW;
   const int env = env0 + lane;
   const long long E = P.E;
-  const bool valid = env < E;
-  const int nenv = (E - env0) < WAVE ? (int)(E - env0) : WAVE;
+  const bool valid = lane < EPW && env < E;
+  const int nenv = (E - env0) < EPW ? (int)(E - env0) : EPW;
   const int A = P.A, nb = P.nb;
-  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16);
+  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
   for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
@@ -998,7 +1031,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   duct_col[lane] = duct;
   __syncthreads();
   if (valid) {
-    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E};
+    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E, max_range2(P, duct)};
     int a0 = 0, a1 = A;
     if (sel >= 0) { a0 = sel; a1 = sel + 1; }
     else if (sel == LNW_OBS_BLUE) { a1 = nb; }
@@ -1278,7 +1311,7 @@ KState make_state(lnw_handle *h) {
 }
 
 size_t step_lds_bytes(const lnw_handle *h, bool march) {
-  LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16);
+  LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G);
   return (size_t)L.total;
 }
 
@@ -1496,7 +1529,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   KState s = make_state(h);
   bool march = k.los_mode == 1;
   size_t lds = step_lds_bytes(h, march);
-  dim3 grid((h->E + WAVE - 1) / WAVE), block(WAVE);
+  dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
   if (march)
     step_kernel<true><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev,
@@ -1515,7 +1548,7 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
   KState s = make_state(h);
   bool march = h->kp.los_mode == 1;
   size_t lds = step_lds_bytes(h, march);
-  dim3 grid((h->E + WAVE - 1) / WAVE), block(WAVE);
+  dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
   if (march)
     observe_kernel<true><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
