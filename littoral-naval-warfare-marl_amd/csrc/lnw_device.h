@@ -70,7 +70,8 @@ struct KState {
   uint8_t *bear_ship;  // [nmax*nmax][E]
   const uint8_t *grid;     // [G][G]
   const float *gridf;      // [G][G] grid/255 as float32
-  const float *winf;       // [G*G][52] Combatant windows | [G*G][28] LandingShip windows
+  const float *winf;       // [2][G*G][52] Combatant | LandingShip observation windows
+  float *dummy;            // [WAVE * 4] sink for masked-out stores (keeps store counts static)
   const uint32_t *mask2;   // [G][W16] 2 bits per cell: bit0 > move_thr, bit1 > ew_thr
   const uint32_t *mvtab;   // [2][G*G][3]
   const uint32_t *lostab;  // [G*G][486]

@@ -26,6 +26,10 @@
 
 using namespace lnw;
 
+// native 4 x f32 vector: arrays of it stay in VGPRs (HIP's union-based float4
+// defeats SROA and lands such arrays in scratch)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 namespace {
 
 #ifndef LNW_EPW
@@ -51,9 +55,8 @@ struct LdsLayout {
 // is a multiple of 4 with S/4 odd: rows are 16-B aligned so the copy-out reads
 // float4s (ds_read_b128, conflict-free), and row starts spread over 8 banks
 // (ds_write_b32 from lanes on different rows is at most 2-way).
-__host__ __device__ inline int stage_stride(int ns) {
-  int D = 4 * ns + 52;
-  return ((D / 4) & 1) ? D : D + 4;
+__host__ __device__ constexpr int stage_stride(int ns) {
+  return (((4 * ns + 52) / 4) & 1) ? (4 * ns + 52) : (4 * ns + 56);
 }
 // Phase-O LDS: staged rows (one pass = the rows of WAVE/A envs) | x/G LUT.
 __host__ __device__ inline int envs_per_pass(int A) { return WAVE / A; }
@@ -212,71 +215,61 @@ __device__ inline uint32_t los_q(const KParams &P, const KState &S, const uint32
 // get_obs sensor fusion (combatant.py:90-161 / landingship.py:94-165): refreshes
 // the target list of agent `me`. Observation floats are written in phase O.
 // ---------------------------------------------------------------------------
-__device__ void get_obs_dev(Ctx &X, int me) {
+struct ObsAcc {
+  int obs_n, norder;
+};
+
+// One own-ship x opponent check of get_obs (combatant.py:106-124) once the
+// squared distance is known: radar / close / EW conditions, LOS (table or
+// march), the position-deduplicated observed list and EW bearings (gauss).
+__device__ inline void pair_detect(Ctx &X, int myradar, int i, int jj, int xi, int yi, int ti,
+                                   int xj, int yj, int tj, int radj, int d2, ObsAcc &acc) {
+  const KParams &P = X.P;
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
+  bool rad_ok = myradar == 1 && d2 < rr * rr;
+  bool close = d2 < 16;
+  bool ew_cand = d2 < re * re && radj == 1;
+  if (!(rad_ok || close || ew_cand)) return;  // LOS result would be unused
+  uint32_t los = los_q(P, S, X.mask, xi, yi, xj, yj);
+  if (!(los & 1u)) return;
+  uint32_t pk = pack_pos(xj, yj);
+  bool seen = false;
+  for (int q = 0; q < acc.obs_n; q++) seen |= COLW(c.observed, q) == pk;
+  if ((rad_ok || close) && !seen) {
+    COLW(c.observed, acc.obs_n) = pk;
+    acc.obs_n++;
+    seen = true;
+  }
+  if (ew_cand && (los & 2u) && !seen) {
+    // calculate_bearing (combatant.py:249-263)
+    double bearing = atan2((double)(yj - yi), (double)(xj - xi)) * RAD2DEG;
+    double distortion = X.rng.gauss();
+    if (bearing + distortion < 0)
+      bearing = bearing + distortion + 360.0;
+    else
+      bearing = bearing + distortion;
+    int k = COLB(c.bcnt, jj);
+    if (k == 0) { COLB(c.border, acc.norder) = (uint8_t)jj; acc.norder++; }
+    size_t slot = (size_t)(jj * S.nmax + k) * X.E + X.env;
+    S.bear_val[slot] = bearing;
+    S.bear_ship[slot] = (uint8_t)i;
+    COLB(c.bcnt, jj) = (uint8_t)(k + 1);
+  }
+}
+
+// Target list (combatant.py:152-161): observed positions first, then every EW
+// fix (combatant.py:128-150) landing within 2 cells of a live opponent.
+__device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsAcc &acc) {
   const KParams &P = X.P;
   const KState &S = X.S;
   Cols &c = X.c;
   const int lane = X.lane;
   const long long E = X.E;
   const int env = X.env;
-  const int nb = P.nb, A = P.A;
-  const int side = me >= nb;
-  const int own0 = side ? nb : 0, own1 = side ? A : nb;
-  const int opp0 = side ? 0 : nb, opp1 = side ? nb : A;
-  const int nopp = opp1 - opp0;
-  const int myradar = COLW(c.radar_cur, me);
-  int obs_n = 0;
-  int norder = 0;
-  for (int q = 0; q < nopp; q++) COLB(c.bcnt, q) = 0;
-
-  for (int i = own0; i < own1; i++) {
-    if (!COLB(c.alive0, i)) continue;
-    uint32_t pi = COLW(c.pos_cur, i);
-    int xi = pos_x(pi), yi = pos_y(pi);
-    int ti = COLB(c.type, i);
-    for (int j = opp0; j < opp1; j++) {
-      if (!COLB(c.alive0, j)) continue;
-      uint32_t pj = COLW(c.pos_cur, j);
-      int xj = pos_x(pj), yj = pos_y(pj);
-      int tj = COLB(c.type, j);
-      int dx = xj - xi, dy = yj - yi;
-      int d2 = dx * dx + dy * dy;
-      if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
-      int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
-      bool rad_ok = myradar == 1 && d2 < rr * rr;
-      bool close = d2 < 16;
-      bool ew_cand = d2 < re * re && COLW(c.radar_cur, j) == 1;
-      if (!(rad_ok || close || ew_cand)) continue;  // LOS result would be unused
-      uint32_t los = los_q(P, S, X.mask, xi, yi, xj, yj);
-      if (!(los & 1u)) continue;
-      uint32_t pk = pj & 0x7fff7fffu;
-      bool seen = false;
-      for (int q = 0; q < obs_n; q++) seen |= COLW(c.observed, q) == pk;
-      if ((rad_ok || close) && !seen) {
-        COLW(c.observed, obs_n) = pk;
-        obs_n++;
-        seen = true;
-      }
-      if (ew_cand && (los & 2u) && !seen) {
-        // calculate_bearing (combatant.py:249-263)
-        double bearing = atan2((double)dy, (double)dx) * RAD2DEG;
-        double distortion = X.rng.gauss();
-        if (bearing + distortion < 0)
-          bearing = bearing + distortion + 360.0;
-        else
-          bearing = bearing + distortion;
-        int jj = j - opp0;
-        int k = COLB(c.bcnt, jj);
-        if (k == 0) { COLB(c.border, norder) = (uint8_t)jj; norder++; }
-        size_t slot = (size_t)(jj * S.nmax + k) * E + env;
-        S.bear_val[slot] = bearing;
-        S.bear_ship[slot] = (uint8_t)i;
-        COLB(c.bcnt, jj) = (uint8_t)(k + 1);
-      }
-    }
-  }
-
-  // target list: observed positions first (combatant.py:152-154)
+  const int obs_n = acc.obs_n, norder = acc.norder;
   const int T = P.T;
   uint16_t *tl = S.tl + (size_t)me * T * E + env;
   int tn = 0;
@@ -374,6 +367,87 @@ __device__ void get_obs_dev(Ctx &X, int me) {
     }
   }
   COLW(c.tcnt, me) = (uint32_t)tn;
+}
+
+
+// get_obs sensor fusion (combatant.py:90-161 / landingship.py:94-165) for
+// runtime ship counts: refreshes agent me's target list (observation floats are
+// written in phase O).
+__device__ void get_obs_dev(Ctx &X, int me) {
+  const KParams &P = X.P;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const int nb = P.nb, A = P.A;
+  const int side = me >= nb;
+  const int own0 = side ? nb : 0, own1 = side ? A : nb;
+  const int opp0 = side ? 0 : nb, opp1 = side ? nb : A;
+  const int myradar = COLW(c.radar_cur, me);
+  ObsAcc acc{0, 0};
+  for (int q = 0; q < opp1 - opp0; q++) COLB(c.bcnt, q) = 0;
+  for (int i = own0; i < own1; i++) {
+    if (!COLB(c.alive0, i)) continue;
+    uint32_t pi = COLW(c.pos_cur, i);
+    int xi = pos_x(pi), yi = pos_y(pi);
+    int ti = COLB(c.type, i);
+    for (int j = opp0; j < opp1; j++) {
+      if (!COLB(c.alive0, j)) continue;
+      uint32_t pj = COLW(c.pos_cur, j);
+      int xj = pos_x(pj), yj = pos_y(pj);
+      int dx = xj - xi, dy = yj - yi;
+      int d2 = dx * dx + dy * dy;
+      if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
+      pair_detect(X, myradar, i, j - opp0, xi, yi, ti, xj, yj, COLB(c.type, j),
+                  COLW(c.radar_cur, j), d2, acc);
+    }
+  }
+  finish_obs(X, me, opp0, opp1, acc);
+}
+
+// Compile-time ship counts: positions and alive flags of both sides are read
+// into registers once, the 16 (4v4) distance tests run branch-free, and only
+// pairs inside a sensor range take the pair_detect path.
+template <int NOWN, int NOPP>
+__device__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const int myradar = COLW(c.radar_cur, me);
+  int xo[NOWN], yo[NOWN];
+  int xp[NOPP], yp[NOPP];
+  uint32_t amask = 0;
+#pragma unroll
+  for (int i = 0; i < NOWN; i++) {
+    uint32_t p = COLW(c.pos_cur, own0 + i);
+    xo[i] = pos_x(p); yo[i] = pos_y(p);
+    amask |= (COLB(c.alive0, own0 + i) ? 1u : 0u) << i;
+  }
+#pragma unroll
+  for (int j = 0; j < NOPP; j++) {
+    uint32_t p = COLW(c.pos_cur, opp0 + j);
+    xp[j] = pos_x(p); yp[j] = pos_y(p);
+    amask |= (COLB(c.alive0, opp0 + j) ? 1u : 0u) << (NOWN + j);
+    COLB(c.bcnt, j) = 0;
+  }
+  uint32_t near = 0;  // bit i*NOPP+j: both alive and within the max sensor range
+#pragma unroll
+  for (int i = 0; i < NOWN; i++)
+#pragma unroll
+    for (int j = 0; j < NOPP; j++) {
+      int dx = xp[j] - xo[i], dy = yp[j] - yo[i];
+      bool in = ((amask >> i) & (amask >> (NOWN + j)) & 1u) && dx * dx + dy * dy < X.r2max;
+      near |= (in ? 1u : 0u) << (i * NOPP + j);
+    }
+  ObsAcc acc{0, 0};
+  while (near) {  // pairs in index order (i outer, j inner), as the reference loops
+    int b = __builtin_ctz(near);
+    near &= near - 1;
+    int i = b / NOPP, j = b - (b / NOPP) * NOPP;
+    uint32_t pi = COLW(c.pos_cur, own0 + i), pj = COLW(c.pos_cur, opp0 + j);
+    int xi = pos_x(pi), yi = pos_y(pi), xj = pos_x(pj), yj = pos_y(pj);
+    int dx = xj - xi, dy = yj - yi;
+    pair_detect(X, myradar, own0 + i, j, xi, yi, COLB(c.type, own0 + i), xj, yj,
+                COLB(c.type, opp0 + j), COLW(c.radar_cur, opp0 + j), dx * dx + dy * dy, acc);
+  }
+  finish_obs(X, me, opp0, opp0 + NOPP, acc);
 }
 
 // check_target (combatant.py:570-584): first live opponent within 3.5 cells
@@ -607,22 +681,22 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
   int idx;
   if (tk == T_LS) {
     // asymmetric 5x5 window rows/cols pos-1..pos+3 (landingship.py:178-188)
-    const float4 *w = (const float4 *)(S.winf + (size_t)G * G * 52 + (size_t)(px * G + py) * 28);
-    float4 v[7];
+    const f32x4 *w = (const f32x4 *)(S.winf + ((size_t)G * G + (size_t)(px * G + py)) * 52);
+    f32x4 v[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) v[q] = w[q];
-    float4 *r4 = (float4 *)row;
+    f32x4 *r4 = (f32x4 *)row;
 #pragma unroll
     for (int q = 0; q < 6; q++) r4[q] = v[q];
     row[24] = v[6].x;
     idx = 25;
   } else {
     // 7x7 window around the ship (combatant.py:174-181)
-    const float4 *w = (const float4 *)(S.winf + (size_t)(px * G + py) * 52);
-    float4 v[13];
+    const f32x4 *w = (const f32x4 *)(S.winf + (size_t)(px * G + py) * 52);
+    f32x4 v[13];
 #pragma unroll
     for (int q = 0; q < 13; q++) v[q] = w[q];
-    float4 *r4 = (float4 *)row;
+    f32x4 *r4 = (f32x4 *)row;
 #pragma unroll
     for (int q = 0; q < 12; q++) r4[q] = v[q];
     row[48] = v[12].x;
@@ -667,8 +741,8 @@ __device__ inline void copy_side(const float *stage, float *out, int ns, int ne,
   const int S4 = stage_stride(ns) >> 2;
   const int D4 = D >> 2;
   const int n4 = ne * ns * D4;
-  const float4 *st4 = (const float4 *)stage;
-  float4 *base = (float4 *)(out + (size_t)genv0 * ns * D);
+  const f32x4 *st4 = (const f32x4 *)stage;
+  f32x4 *base = (f32x4 *)(out + (size_t)genv0 * ns * D);
   int r = lane / D4, c4 = lane - r * D4;
   for (int i = lane; i < n4; i += WAVE) {
     base[i] = st4[r * S4 + c4];
@@ -711,6 +785,138 @@ __device__ void write_obs(const KParams &P, const KState &S, Cols &c, const doub
   }
 }
 
+// Compile-time shapes: the copy-out is fully unrolled (the compiler then knows
+// how many stores follow the prefetched window loads), and the next pass's
+// window loads are issued before this pass's stores, so waiting for them never
+// drains the stores (vmcnt counts loads and stores together in issue order).
+template <int NS>
+__device__ inline void row_tail(const Cols &c, const double *duct_col, int el, int k, int own0,
+                                int tk, int px, int py, float *row, int idx, const float *xg) {
+  constexpr int D = 4 * NS + 52;
+  const int kl = k - own0;
+  row[idx++] = xg[px];
+  row[idx++] = xg[py];
+  row[idx++] = (float)c.radar_cur[k * PAD + el];
+  row[idx++] = (float)c.miss_cur[k * PADB + el] * (tk == T_SMALL ? 0.25f : 0.125f);
+#pragma unroll
+  for (int il = 0; il < NS; il++) {
+    if (il == kl) continue;
+    const int i = own0 + il;
+    if (c.alive0[i * PADB + el]) {
+      const bool nw = il < kl;  // own ships that acted before k show their new state
+      const uint32_t q = nw ? c.pos_cur[i * PAD + el] : c.pos_old[i * PAD + el];
+      row[idx] = xg[pos_x(q)];
+      row[idx + 1] = xg[pos_y(q)];
+      row[idx + 2] = (float)(nw ? c.radar_cur[i * PAD + el] : c.radar_old[i * PAD + el]);
+      const int m = nw ? c.miss_cur[i * PADB + el] : c.miss_old[i * PADB + el];
+      row[idx + 3] = (float)m * (c.type[i * PADB + el] == T_SMALL ? 0.25f : 0.125f);
+    } else {
+      row[idx] = row[idx + 1] = row[idx + 2] = row[idx + 3] = 0.0f;
+    }
+    idx += 4;
+  }
+  row[idx++] = (float)c.tcnt[k * PAD + el];
+  row[idx++] = tk == T_LS ? 1.0f : 0.0f;
+  row[idx++] = (float)(duct_col[el] / 2.0);
+  for (; idx < D; idx++) row[idx] = 0.0f;
+}
+
+template <int NS, int NPASS4>
+__device__ inline void copy_side_t(const float *stage, float *out, float *dummy, int ne,
+                                   long long genv0) {
+  constexpr int D = 4 * NS + 52, D4 = D / 4, S4 = stage_stride(NS) / 4;
+  constexpr int IT = (NPASS4 + WAVE - 1) / WAVE;
+  const int lane = threadIdx.x;
+  const int n4 = ne * NS * D4;
+  const f32x4 *st4 = (const f32x4 *)stage;
+  f32x4 *base = (f32x4 *)(out + (size_t)genv0 * NS * D);
+  f32x4 v[IT];
+#pragma unroll
+  for (int u = 0; u < IT; u++) {  // all LDS reads first (no per-element branch)
+    int i = lane + u * WAVE;
+    i = i < n4 ? i : n4 - 1;
+    const int r = i / D4, c4 = i - (i / D4) * D4;
+    v[u] = st4[r * S4 + c4];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < IT; u++) {  // unconditional stores: masked-out lanes hit the sink
+    const int i = lane + u * WAVE;
+    f32x4 *dst = i < n4 ? base + i : (f32x4 *)dummy + lane;
+    *dst = v[u];
+  }
+}
+
+template <int NB, int NR>
+__device__ void write_obs_t(const KParams &P, const KState &S, Cols &c, const double *duct_col,
+                            float *obs_b, float *obs_r, int env0, int nenv) {
+  constexpr int A = NB + NR, EPG = WAVE / A;
+  const int lane = threadIdx.x;
+  const int my_e = lane / A, my_k = lane - (lane / A) * A;
+  const int side = my_k >= NB;
+  const int own0 = side ? NB : 0;
+  const int kl = my_k - own0;
+  const int G = P.G;
+  float *stage_b = c.stage;
+  float *stage_r = c.stage + EPG * NB * stage_stride(NB);
+  float *row = side ? stage_r + (my_e * NR + kl) * stage_stride(NR)
+                    : stage_b + (my_e * NB + kl) * stage_stride(NB);
+  float *xg = stage_r + EPG * NR * stage_stride(NR);
+  for (int x = lane; x < G; x += WAVE) xg[x] = (float)((double)x / (double)G);
+  const f32x4 *wtab = (const f32x4 *)S.winf;
+  f32x4 v[12];
+  float w48;
+  // 12 unconditional float4 loads + 1 float of the row's window record (a dead
+  // or absent row loads cell 0's record and ignores it)
+  auto prefetch = [&](int g0) {
+    const int el = g0 + my_e;
+    int off = 0;
+    if (my_e < EPG && el < nenv) {
+      const uint32_t p = c.pos_cur[my_k * PAD + el];
+      off = ((c.type[my_k * PADB + el] == T_LS ? G * G : 0) + pos_x(p) * G + pos_y(p)) * 13;
+    }
+#pragma unroll
+    for (int q = 0; q < 12; q++) v[q] = wtab[off + q];
+    w48 = ((const float *)(wtab + off))[48];
+  };
+  prefetch(0);
+  wave_lds_sync();
+  for (int g0 = 0; g0 < nenv; g0 += EPG) {
+    const int ne = (nenv - g0) < EPG ? (nenv - g0) : EPG;
+    if (my_e < ne) {
+      const int el = g0 + my_e;
+      constexpr int DB = 4 * NB + 52, DR = 4 * NR + 52;
+      if (!c.alive0[my_k * PADB + el]) {
+        const int D = side ? DR : DB;
+        for (int d = 0; d < D; d++) row[d] = 0.0f;
+      } else {
+        const uint32_t p = c.pos_cur[my_k * PAD + el];
+        const int tk = c.type[my_k * PADB + el];
+        f32x4 *r4 = (f32x4 *)row;
+        int idx;
+        if (tk == T_LS) {
+#pragma unroll
+          for (int q = 0; q < 6; q++) r4[q] = v[q];
+          row[24] = v[6].x;
+          idx = 25;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 12; q++) r4[q] = v[q];
+          row[48] = w48;
+          idx = 49;
+        }
+        if (side) row_tail<NR>(c, duct_col, el, my_k, own0, tk, pos_x(p), pos_y(p), row, idx, xg);
+        else row_tail<NB>(c, duct_col, el, my_k, own0, tk, pos_x(p), pos_y(p), row, idx, xg);
+      }
+    }
+    wave_lds_sync();
+    if (g0 + EPG < nenv) prefetch(g0 + EPG);
+    copy_side_t<NB, EPG * NB * (4 * NB + 52) / 4>(stage_b, obs_b, S.dummy, ne, env0 + g0);
+    copy_side_t<NR, EPG * NR * (4 * NR + 52) / 4>(stage_r, obs_r, S.dummy, ne, env0 + g0);
+    wave_lds_sync();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // phase L: load state columns
 // ---------------------------------------------------------------------------
@@ -749,7 +955,9 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // ---------------------------------------------------------------------------
 // step kernel (Game.step, game.py:298-525)
 // ---------------------------------------------------------------------------
-template <bool MARCH>
+// NB/NR > 0: compile-time ship counts (register pair loop in get_obs, unrolled
+// observation copy-out); NB = NR = 0: runtime counts from P.
+template <int NB, int NR>
 __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *actions,
                                                   const uint8_t *row_kind, float *obs_b,
                                                   float *obs_r, float *rew_b, float *rew_r,
@@ -760,8 +968,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   const long long E = P.E;
   const bool valid = lane < EPW && env < E;
   const int nenv = (E - env0) < EPW ? (int)(E - env0) : EPW;
-  const int A = P.A, nb = P.nb, nr = P.nr;
-  LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16, P.G);
+  constexpr bool ST = NB > 0;
+  const int nb = ST ? NB : P.nb, nr = ST ? NR : P.nr;
+  const int A = nb + nr;
+  LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
 
@@ -796,7 +1006,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
         double a2, a3;
         int kind;
         if (dt == LNW_ACT_F32) {
-          float4 v = *(const float4 *)((const float *)actions + row);
+          f32x4 v = *(const f32x4 *)((const float *)actions + row);
           COLW(c.act0, a) = v.x;
           COLW(c.act1, a) = v.y;
           a2 = v.z;
@@ -897,7 +1107,12 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
       uint32_t pn = COLW(c.pos_new, a);
       bool moved = (pn & 0x80000000u) != 0;
       if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
-      get_obs_dev(X, a);
+      if constexpr (ST) {
+        if (!side) get_obs_t<NB, NR>(X, a, 0, NB);
+        else get_obs_t<NR, NB>(X, a, NB, 0);
+      } else {
+        get_obs_dev(X, a);
+      }
       double r = reward_dev(X, a, moved, engage, destroyed);
       COLW(c.reward, a) = r;
       if (!side) {
@@ -1005,13 +1220,13 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   __syncthreads();
   // ---- phase O: observations ---------------------------------------------
   if (P.dbg_skip & 1) return;
-  write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
+  if constexpr (ST) write_obs_t<NB, NR>(P, S, c, duct_col, obs_b, obs_r, env0, nenv);
+  else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
 }
 
 // ---------------------------------------------------------------------------
 // observe kernel (ship.get_obs() for a selection of ships)
 // ---------------------------------------------------------------------------
-template <bool MARCH>
 __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
                                                      float *obs_r) {
   const int lane = threadIdx.x;
@@ -1267,7 +1482,7 @@ struct lnw_handle {
   bool terrain = false;
   // device buffers
   uint8_t *d_grid = nullptr;
-  float *d_gridf = nullptr, *d_winf = nullptr;
+  float *d_gridf = nullptr, *d_winf = nullptr, *d_dummy = nullptr;
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -1302,7 +1517,7 @@ KState make_state(lnw_handle *h) {
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
   s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
-  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
   s.sp_pos_env = nullptr;
@@ -1310,7 +1525,7 @@ KState make_state(lnw_handle *h) {
   return s;
 }
 
-size_t step_lds_bytes(const lnw_handle *h, bool march) {
+size_t step_lds_bytes(const lnw_handle *h) {
   LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G);
   return (size_t)L.total;
 }
@@ -1368,6 +1583,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   rc |= dalloc(h, &h->sp_types, 64);
   rc |= dalloc(h, &h->sp_pos, 128);
   rc |= dalloc(h, &h->sp_randls, 64);
+  rc |= dalloc(h, &h->d_dummy, 4 * 64);
   if (rc) {
     std::string m = g_err;
     lnw_destroy(h);
@@ -1415,7 +1631,7 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   }
   rc |= dalloc(h, &h->d_grid, (size_t)G * G);
   rc |= dalloc(h, &h->d_gridf, (size_t)G * G);
-  rc |= dalloc(h, &h->d_winf, (size_t)G * G * (52 + 28));
+  rc |= dalloc(h, &h->d_winf, (size_t)2 * G * G * 52);
   rc |= dalloc(h, &h->d_mask2, (size_t)G * h->W16);
   rc |= dalloc(h, &h->d_mvtab, (size_t)2 * G * G * MV_WORDS);
   rc |= dalloc(h, &h->d_lostab, (size_t)G * G * LOS_CELL_WORDS);
@@ -1425,10 +1641,11 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     std::vector<float> gf((size_t)G * G);
     for (size_t i = 0; i < gf.size(); i++) gf[i] = (float)((double)grid_host[i] / 255.0);
     HIPCHK(hipMemcpy(h->d_gridf, gf.data(), gf.size() * sizeof(float), hipMemcpyHostToDevice));
-    // per-cell observation windows: Combatant 7x7 around the ship (49 floats,
-    // padded to 52), LandingShip 5x5 rows/cols pos-1..pos+3 (25, padded to 28);
-    // cells outside the hard-coded 0..99 are 0 (combatant.py:176)
-    std::vector<float> wf((size_t)G * G * (52 + 28), 0.0f);
+    // per-cell observation windows, one 52-float (13 x float4) record per cell
+    // and class: [0] Combatant 7x7 around the ship (49 floats), [1] LandingShip
+    // 5x5 rows/cols pos-1..pos+3 (25 floats); cells outside the hard-coded
+    // 0..99 are 0 (combatant.py:176, landingship.py:183)
+    std::vector<float> wf((size_t)2 * G * G * 52, 0.0f);
     auto cellv = [&](int x, int y) {
       return (0 <= x && x < 100 && 0 <= y && y < 100 && x < G && y < G) ? gf[(size_t)x * G + y] : 0.0f;
     };
@@ -1437,7 +1654,7 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
         float *w7 = &wf[((size_t)x * G + y) * 52];
         for (int i = 0; i < 7; i++)
           for (int j = 0; j < 7; j++) w7[i * 7 + j] = cellv(x - 3 + i, y - 3 + j);
-        float *w5 = &wf[(size_t)G * G * 52 + ((size_t)x * G + y) * 28];
+        float *w5 = &wf[((size_t)G * G + (size_t)x * G + y) * 52];
         for (int i = 0; i < 5; i++)
           for (int j = 0; j < 5; j++) w5[i * 5 + j] = cellv(x - 1 + i, y - 1 + j);
       }
@@ -1458,13 +1675,15 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   HIPCHK(hipDeviceSynchronize());
   h->terrain = true;
   // dynamic LDS above the 64 KiB default needs an explicit opt-in
-  for (int m = 0; m < 2; m++) {
-    size_t need = step_lds_bytes(h, m == 1) + 1024;
+  {
+    size_t need = step_lds_bytes(h) + 1024;
+    if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     if (need > 64 * 1024) {
-      if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
-      const void *ks[2] = {m ? (const void *)step_kernel<true> : (const void *)step_kernel<false>,
-                           m ? (const void *)observe_kernel<true> : (const void *)observe_kernel<false>};
-      for (const void *k : ks) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+      const void *ks[5] = {(const void *)step_kernel<0, 0>, (const void *)step_kernel<2, 2>,
+                           (const void *)step_kernel<3, 3>, (const void *)step_kernel<4, 4>,
+                           (const void *)observe_kernel};
+      for (const void *kk : ks)
+        HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
     }
   }
   (void)hipGetLastError();
@@ -1527,16 +1746,19 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   k.act_dtype = action_dtype;
   if (const char *dbg = getenv("LNW_DEBUG_SKIP")) k.dbg_skip = atoi(dbg);
   KState s = make_state(h);
-  bool march = k.los_mode == 1;
-  size_t lds = step_lds_bytes(h, march);
+  size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
-  if (march)
-    step_kernel<true><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev,
-                                               obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
-  else
-    step_kernel<false><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev,
-                                                obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
+  bool generic = getenv("LNW_FORCE_GENERIC") != nullptr;
+#define LNW_STEP(NB_, NR_)                                                                       \
+  step_kernel<NB_, NR_><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
+                                                 obs_red_dev, rew_blue_dev, rew_red_dev,        \
+                                                 done_dev, cog_dev)
+  if (!generic && h->nb == 4 && h->nr == 4) LNW_STEP(4, 4);
+  else if (!generic && h->nb == 3 && h->nr == 3) LNW_STEP(3, 3);
+  else if (!generic && h->nb == 2 && h->nr == 2) LNW_STEP(2, 2);
+  else LNW_STEP(0, 0);
+#undef LNW_STEP
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1546,14 +1768,9 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
   if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
   if (agent >= h->A || agent < LNW_OBS_RED) return fail(LNW_EINVAL, "bad agent selector");
   KState s = make_state(h);
-  bool march = h->kp.los_mode == 1;
-  size_t lds = step_lds_bytes(h, march);
+  size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
-  hipStream_t st = (hipStream_t)stream;
-  if (march)
-    observe_kernel<true><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
-  else
-    observe_kernel<false><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
+  observe_kernel<<<grid, block, lds, (hipStream_t)stream>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
   HIPCHK(hipGetLastError());
   return 0;
 }
