@@ -48,7 +48,9 @@ struct LdsLayout {
   // phase-S scratch (dead before phase O) ...
   int pos_new, reward, observed, open, mkind, eng, bcnt, border, steps, act0, act1, akind;
   // ... aliased by the phase-O row staging area
-  int stage, mask, total;
+  int stage;
+  // terrain mask (phase M), aliased in phase S by the row-emission stage
+  int mask, estage, total;
 };
 
 // Row staging for phase O: up to 64 observation rows. The row stride S (floats)
@@ -67,6 +69,11 @@ __host__ __device__ inline int stage_rows_bytes(int A, int nb, int nr) {
 __host__ __device__ inline int stage_bytes(int A, int nb, int nr, int G) {
   return stage_rows_bytes(A, nb, nr) + ((G + 3) & ~3) * 4;
 }
+
+// Phase-S row emission (emit_rows_t): one group of row chunks for the 64 envs
+// (row stride EST4 float4s, odd: conflict-free ds_write_b128) | x/G LUT.
+constexpr int EST4 = 5;
+__host__ __device__ inline int estage_bytes(int G) { return WAVE * EST4 * 16 + ((G + 3) & ~3) * 4; }
 
 __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax, int mask_words,
                                                 int G) {
@@ -103,7 +110,9 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   int st_end = scratch + stage_bytes(A, nb, nr, G);
   if (st_end > o) o = st_end;
   o = (o + 15) & ~15;
-  L.mask = o; o += mask_words * 4;
+  L.mask = o;
+  L.estage = o;
+  o += mask_words * 4 > estage_bytes(G) ? mask_words * 4 : estage_bytes(G);
   L.total = o;
   return L;
 }
@@ -114,7 +123,7 @@ struct Cols {
   double *reward, *act0, *act1;
   uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border, *akind;
   uint32_t *mask;
-  float *stage;
+  float *stage, *estage;
 };
 
 __device__ inline Cols carve(char *base, const LdsLayout &L) {
@@ -143,6 +152,7 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
   c.border = (uint8_t *)(base + L.border);
   c.mask = (uint32_t *)(base + L.mask);
   c.stage = (float *)(base + L.stage);
+  c.estage = (float *)(base + L.estage);
   return c;
 }
 
@@ -373,7 +383,7 @@ __device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsA
 // get_obs sensor fusion (combatant.py:90-161 / landingship.py:94-165) for
 // runtime ship counts: refreshes agent me's target list (observation floats are
 // written in phase O).
-__device__ void get_obs_dev(Ctx &X, int me) {
+__device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   const KParams &P = X.P;
   Cols &c = X.c;
   const int lane = X.lane;
@@ -407,7 +417,7 @@ __device__ void get_obs_dev(Ctx &X, int me) {
 // into registers once, the 16 (4v4) distance tests run branch-free, and only
 // pairs inside a sensor range take the pair_detect path.
 template <int NOWN, int NOPP>
-__device__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
+__device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
   Cols &c = X.c;
   const int lane = X.lane;
   const int myradar = COLW(c.radar_cur, me);
@@ -574,7 +584,7 @@ __device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int 
 }
 
 // Game.reset for one env (game.py:528-613), in-kernel
-__device__ void reset_env_dev(const KParams &P, const KState &S, int env, Rng &rng) {
+__device__ __forceinline__ void reset_env_dev(const KParams &P, const KState &S, int env, Rng &rng) {
   const long long E = P.E;
   double duct = 1.0 + rng.beta13();
   S.duct[env] = duct;
@@ -663,7 +673,7 @@ __device__ inline Rng make_rng(const KParams &P, const KState &S, int env) {
 // a ds_write_b32 across lanes is conflict-free). The terrain window comes from
 // the per-cell window table (Combatant 49 floats padded to 52, LandingShip 25
 // padded to 28): 13 / 7 independent float4 loads issued together.
-__device__ void build_row(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
+__device__ __forceinline__ void build_row(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
                           int el, int k, float *row, const float *xg, bool only_observed) {
   const int side = k >= P.nb;
   const int own0 = side ? P.nb : 0;
@@ -736,7 +746,7 @@ __device__ void build_row(const KParams &P, const KState &S, const Cols &c, cons
 // (1 KiB per wave store instruction).
 __device__ inline void copy_side(const float *stage, float *out, int ns, int ne, long long genv0) {
   if (!out) return;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int D = 4 * ns + 52;
   const int S4 = stage_stride(ns) >> 2;
   const int D4 = D >> 2;
@@ -757,9 +767,9 @@ __device__ inline void copy_side(const float *stage, float *out, int ns, int ne,
 // global store (s_waitcnt vmcnt(0)) each group.
 __device__ inline void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ void write_obs(const KParams &P, const KState &S, Cols &c, const double *duct_col,
+__device__ __forceinline__ void write_obs(const KParams &P, const KState &S, Cols &c, const double *duct_col,
                           float *obs_b, float *obs_r, int env0, int nenv, bool only_observed) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int A = P.A, nb = P.nb, nr = P.nr;
   const int epg = envs_per_pass(A);
   const int my_e = lane / A, my_k = lane - (lane / A) * A;
@@ -789,36 +799,67 @@ __device__ void write_obs(const KParams &P, const KState &S, Cols &c, const doub
 // how many stores follow the prefetched window loads), and the next pass's
 // window loads are issued before this pass's stores, so waiting for them never
 // drains the stores (vmcnt counts loads and stores together in issue order).
+// One observation row assembled in registers (same content as build_row):
+// every LDS read is issued up front without branches, teammate slot s holds
+// own ship s < kl ? s : s + 1 (combatant.py:190-212), and the row leaves as
+// D/4 ds_write_b128. Combatant rows: window[49] | tail; LandingShip rows:
+// window[25] | tail | zeros (the LS window record is zero past 25 floats).
 template <int NS>
-__device__ inline void row_tail(const Cols &c, const double *duct_col, int el, int k, int own0,
-                                int tk, int px, int py, float *row, int idx, const float *xg) {
-  constexpr int D = 4 * NS + 52;
+__device__ inline void row_regs_t(const Cols &c, const double *duct_col, int el, int k, int own0,
+                                  const f32x4 (&v)[12], float w48, float *row, const float *xg) {
+  constexpr int D = 4 * NS + 52, T = 4 * NS + 3;
   const int kl = k - own0;
-  row[idx++] = xg[px];
-  row[idx++] = xg[py];
-  row[idx++] = (float)c.radar_cur[k * PAD + el];
-  row[idx++] = (float)c.miss_cur[k * PADB + el] * (tk == T_SMALL ? 0.25f : 0.125f);
+  const uint32_t p = c.pos_cur[k * PAD + el];
+  const int tk = c.type[k * PADB + el];
+  const int alive = c.alive0[k * PADB + el];
+  const int rad = c.radar_cur[k * PAD + el];
+  const int mis = c.miss_cur[k * PADB + el];
+  const uint32_t tcn = c.tcnt[k * PAD + el];
+  const double du = duct_col[el];
+  uint32_t tq[NS - 1];
+  int tr[NS - 1], tm[NS - 1], tt[NS - 1], ta[NS - 1];
 #pragma unroll
-  for (int il = 0; il < NS; il++) {
-    if (il == kl) continue;
-    const int i = own0 + il;
-    if (c.alive0[i * PADB + el]) {
-      const bool nw = il < kl;  // own ships that acted before k show their new state
-      const uint32_t q = nw ? c.pos_cur[i * PAD + el] : c.pos_old[i * PAD + el];
-      row[idx] = xg[pos_x(q)];
-      row[idx + 1] = xg[pos_y(q)];
-      row[idx + 2] = (float)(nw ? c.radar_cur[i * PAD + el] : c.radar_old[i * PAD + el]);
-      const int m = nw ? c.miss_cur[i * PADB + el] : c.miss_old[i * PADB + el];
-      row[idx + 3] = (float)m * (c.type[i * PADB + el] == T_SMALL ? 0.25f : 0.125f);
-    } else {
-      row[idx] = row[idx + 1] = row[idx + 2] = row[idx + 3] = 0.0f;
-    }
-    idx += 4;
+  for (int s = 0; s < NS - 1; s++) {
+    const bool nw = s < kl;  // own ships that acted before k show their new state
+    const int i = own0 + (nw ? s : s + 1);
+    tq[s] = (nw ? c.pos_cur : c.pos_old)[i * PAD + el];
+    tr[s] = (nw ? c.radar_cur : c.radar_old)[i * PAD + el];
+    tm[s] = (nw ? c.miss_cur : c.miss_old)[i * PADB + el];
+    tt[s] = c.type[i * PADB + el];
+    ta[s] = c.alive0[i * PADB + el];
   }
-  row[idx++] = (float)c.tcnt[k * PAD + el];
-  row[idx++] = tk == T_LS ? 1.0f : 0.0f;
-  row[idx++] = (float)(duct_col[el] / 2.0);
-  for (; idx < D; idx++) row[idx] = 0.0f;
+  float t[T];
+  t[0] = xg[pos_x(p)];
+  t[1] = xg[pos_y(p)];
+  t[2] = (float)rad;
+  t[3] = (float)mis * (tk == T_SMALL ? 0.25f : 0.125f);
+#pragma unroll
+  for (int s = 0; s < NS - 1; s++) {
+    const float fx = xg[pos_x(tq[s])], fy = xg[pos_y(tq[s])];
+    const float fm = (float)tm[s] * (tt[s] == T_SMALL ? 0.25f : 0.125f);
+    t[4 + 4 * s] = ta[s] ? fx : 0.0f;
+    t[5 + 4 * s] = ta[s] ? fy : 0.0f;
+    t[6 + 4 * s] = ta[s] ? (float)tr[s] : 0.0f;
+    t[7 + 4 * s] = ta[s] ? fm : 0.0f;
+  }
+  t[T - 3] = (float)tcn;
+  t[T - 2] = tk == T_LS ? 1.0f : 0.0f;
+  t[T - 1] = (float)(du / 2.0);
+  const bool ls = tk == T_LS;
+  f32x4 *r4 = (f32x4 *)row;
+#pragma unroll
+  for (int q = 0; q < D / 4; q++) {
+    f32x4 o;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = 4 * q + u;
+      const float w = j < 48 ? v[j >> 2][j & 3] : (j == 48 ? w48 : 0.0f);
+      const float xc = j < 49 ? w : t[j - 49 < T ? j - 49 : 0];
+      const float xl = j < 25 ? w : (j - 25 < T ? t[j - 25 < T ? j - 25 : 0] : 0.0f);
+      o[u] = alive ? (ls ? xl : xc) : 0.0f;
+    }
+    r4[q] = o;
+  }
 }
 
 template <int NS, int NPASS4>
@@ -826,7 +867,7 @@ __device__ inline void copy_side_t(const float *stage, float *out, float *dummy,
                                    long long genv0) {
   constexpr int D = 4 * NS + 52, D4 = D / 4, S4 = stage_stride(NS) / 4;
   constexpr int IT = (NPASS4 + WAVE - 1) / WAVE;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int n4 = ne * NS * D4;
   const f32x4 *st4 = (const f32x4 *)stage;
   f32x4 *base = (f32x4 *)(out + (size_t)genv0 * NS * D);
@@ -843,15 +884,16 @@ __device__ inline void copy_side_t(const float *stage, float *out, float *dummy,
   for (int u = 0; u < IT; u++) {  // unconditional stores: masked-out lanes hit the sink
     const int i = lane + u * WAVE;
     f32x4 *dst = i < n4 ? base + i : (f32x4 *)dummy + lane;
-    *dst = v[u];
+    __builtin_nontemporal_store(v[u], dst);  // streamed out, not re-read by the kernel
   }
 }
 
 template <int NB, int NR>
-__device__ void write_obs_t(const KParams &P, const KState &S, Cols &c, const double *duct_col,
+__device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, Cols &c, const double *duct_col,
                             float *obs_b, float *obs_r, int env0, int nenv) {
+  static_assert(NB == NR, "templated obs rows assume equal team sizes");
   constexpr int A = NB + NR, EPG = WAVE / A;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int my_e = lane / A, my_k = lane - (lane / A) * A;
   const int side = my_k >= NB;
   const int own0 = side ? NB : 0;
@@ -883,47 +925,176 @@ __device__ void write_obs_t(const KParams &P, const KState &S, Cols &c, const do
   wave_lds_sync();
   for (int g0 = 0; g0 < nenv; g0 += EPG) {
     const int ne = (nenv - g0) < EPG ? (nenv - g0) : EPG;
-    if (my_e < ne) {
-      const int el = g0 + my_e;
-      constexpr int DB = 4 * NB + 52, DR = 4 * NR + 52;
-      if (!c.alive0[my_k * PADB + el]) {
-        const int D = side ? DR : DB;
-        for (int d = 0; d < D; d++) row[d] = 0.0f;
-      } else {
-        const uint32_t p = c.pos_cur[my_k * PAD + el];
-        const int tk = c.type[my_k * PADB + el];
-        f32x4 *r4 = (f32x4 *)row;
-        int idx;
-        if (tk == T_LS) {
-#pragma unroll
-          for (int q = 0; q < 6; q++) r4[q] = v[q];
-          row[24] = v[6].x;
-          idx = 25;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 12; q++) r4[q] = v[q];
-          row[48] = w48;
-          idx = 49;
-        }
-        if (side) row_tail<NR>(c, duct_col, el, my_k, own0, tk, pos_x(p), pos_y(p), row, idx, xg);
-        else row_tail<NB>(c, duct_col, el, my_k, own0, tk, pos_x(p), pos_y(p), row, idx, xg);
-      }
-    }
+    if (my_e < ne && !(P.dbg_skip & 8))
+      row_regs_t<NB>(c, duct_col, g0 + my_e, my_k, own0, v, w48, row, xg);
     wave_lds_sync();
     if (g0 + EPG < nenv) prefetch(g0 + EPG);
-    copy_side_t<NB, EPG * NB * (4 * NB + 52) / 4>(stage_b, obs_b, S.dummy, ne, env0 + g0);
-    copy_side_t<NR, EPG * NR * (4 * NR + 52) / 4>(stage_r, obs_r, S.dummy, ne, env0 + g0);
+    if (!(P.dbg_skip & 16)) {
+      copy_side_t<NB, EPG * NB * (4 * NB + 52) / 4>(stage_b, obs_b, S.dummy, ne, env0 + g0);
+      copy_side_t<NR, EPG * NR * (4 * NR + 52) / 4>(stage_r, obs_r, S.dummy, ne, env0 + g0);
+    }
     wave_lds_sync();
+  }
+}
+
+// Phase-S row emission (templated equal team sizes, full wave, LOS table
+// mode): Game.step stores ship a's observation as take_action returns it
+// (game.py:343-344, 380-381), so row a of all 64 envs is final right after
+// agent a's turn: own state, teammates before a in their new (*_cur) and
+// teammates after a in their old (*_old) state, the same content write_obs_t
+// builds after the loop. Each row leaves in four chunk groups ({5,4,4,4}
+// float4s) staged through estage.
+// Window record of agent a at its position after phase M's move (pos_new when
+// flagged, else unchanged): known before phase S reaches a, so wave 1 loads it
+// one agent ahead, before the previous agent's stores.
+__device__ inline int window_rec(const KParams &P, const Cols &c, int a, int el) {
+  if (!c.alive0[a * PADB + el]) return 0;
+  const uint32_t pn = c.pos_new[a * PAD + el];
+  const uint32_t p = (pn & 0x80000000u) ? (pn & 0x7fffffffu) : c.pos_old[a * PAD + el];
+  return ((c.type[a * PADB + el] == T_LS ? P.G * P.G : 0) + pos_x(p) * P.G + pos_y(p)) * 13;
+}
+
+__device__ inline void load_window(const KState &S, int off, f32x4 (&v)[12], float &w48) {
+  const f32x4 *rec = (const f32x4 *)S.winf + off;
+#pragma unroll
+  for (int q = 0; q < 12; q++) v[q] = rec[q];
+  w48 = ((const float *)rec)[48];
+}
+
+template <int NS>
+__device__ __forceinline__ void emit_rows_t(const KParams &P, const KState &S, const Cols &c,
+                            const double *duct_col, int a, float *obs_side, int env0,
+                            f32x4 (&v)[12], float &w48) {
+  constexpr int D4 = (4 * NS + 52) / 4, T = 4 * NS + 3;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int el = lane;
+  const int own0 = a >= NS ? NS : 0, kl = a - own0;
+  const int G = P.G;
+  const float *xg = c.estage + WAVE * EST4 * 4;
+  const uint32_t p = c.pos_cur[a * PAD + el];
+  const int tk = c.type[a * PADB + el];
+  const int alive = c.alive0[a * PADB + el];
+  const int rad = c.radar_cur[a * PAD + el];
+  const int mis = c.miss_cur[a * PADB + el];
+  const uint32_t tcn = c.tcnt[a * PAD + el];
+  const double du = duct_col[el];
+  float t[T];
+  t[0] = xg[pos_x(p)];
+  t[1] = xg[pos_y(p)];
+  t[2] = (float)rad;
+  t[3] = (float)mis * (tk == T_SMALL ? 0.25f : 0.125f);
+#pragma unroll
+  for (int s = 0; s < NS - 1; s++) {
+    // teammates before a: new state; after a: the old columns (wave 0 may
+    // already have moved them by the time this row is emitted)
+    const bool nw = s < kl;
+    const int i = own0 + (nw ? s : s + 1);
+    const uint32_t q = (nw ? c.pos_cur : c.pos_old)[i * PAD + el];
+    const int ta = c.alive0[i * PADB + el];
+    const int m = (nw ? c.miss_cur : c.miss_old)[i * PADB + el];
+    const float fm = (float)m * (c.type[i * PADB + el] == T_SMALL ? 0.25f : 0.125f);
+    t[4 + 4 * s] = ta ? xg[pos_x(q)] : 0.0f;
+    t[5 + 4 * s] = ta ? xg[pos_y(q)] : 0.0f;
+    t[6 + 4 * s] = ta ? (float)(nw ? c.radar_cur : c.radar_old)[i * PAD + el] : 0.0f;
+    t[7 + 4 * s] = ta ? fm : 0.0f;
+  }
+  t[T - 3] = (float)tcn;
+  t[T - 2] = tk == T_LS ? 1.0f : 0.0f;
+  t[T - 1] = (float)(du / 2.0);
+  const bool ls = tk == T_LS;
+  f32x4 vc[12];
+#pragma unroll
+  for (int q = 0; q < 12; q++) vc[q] = v[q];
+  const float wc = w48;
+  if (a + 1 < 2 * NS) load_window(S, window_rec(P, c, a + 1, el), v, w48);
+  f32x4 *st4 = (f32x4 *)c.estage;
+  f32x4 *out4 = (f32x4 *)obs_side + ((size_t)env0 * NS + kl) * D4;
+  constexpr int GB[5] = {0, 5, 9, 13, D4};
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const int n = GB[g + 1] - GB[g];
+#pragma unroll
+    for (int u = 0; u < EST4; u++) {
+      if (u >= n) break;
+      const int q = GB[g] + u;
+      f32x4 o;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const int j = 4 * q + w;
+        const float wv = j < 48 ? vc[j >> 2][j & 3] : (j == 48 ? wc : 0.0f);
+        const float xc = j < 49 ? wv : t[j - 49 < T ? j - 49 : 0];
+        const float xl = j < 25 ? wv : (j - 25 < T ? t[j - 25 < T ? j - 25 : 0] : 0.0f);
+        o[w] = alive ? (ls ? xl : xc) : 0.0f;
+      }
+      st4[lane * EST4 + u] = o;
+    }
+    wave_lds_sync();
+    f32x4 cv[EST4];
+#pragma unroll
+    for (int it = 0; it < EST4; it++) {
+      if (it >= n) break;
+      const int i = it * WAVE + lane;
+      const int r = i / n, cc = i - (i / n) * n;
+      cv[it] = st4[r * EST4 + cc];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int it = 0; it < EST4; it++) {
+      if (it >= n) break;
+      const int i = it * WAVE + lane;
+      const int r = i / n, cc = i - (i / n) * n;
+      f32x4 *dst = out4 + (size_t)r * NS * D4 + GB[g] + cc;
+      if (P.dbg_skip & 32) continue;
+      if (P.dbg_skip & 64) *dst = cv[it];
+      else __builtin_nontemporal_store(cv[it], dst);
+    }
+  }
+}
+
+// Wave 1 of a templated step workgroup: emits agent a's rows once wave 0 has
+// published progress > a (LDS counter, -1 until phase S starts: the emission
+// stage aliases the terrain mask phase M reads). Its stores count on its own
+// vmcnt, so wave 0's loads in phase S never wait behind observation stores.
+__device__ inline int wait_progress(const int *prog, int want) {
+  int v;
+  while ((v = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < want)
+    __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+  return v;
+}
+
+__device__ inline void publish_progress(int *prog, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row inputs written before the count
+  __hip_atomic_store(prog, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int NS>
+__device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
+                            const int *prog, float *obs_b, float *obs_r, int env0) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  wait_progress(prog, 0);
+  float *xg = c.estage + WAVE * EST4 * 4;
+  for (int x = lane; x < P.G; x += WAVE) xg[x] = (float)((double)x / (double)P.G);
+  f32x4 v[12];
+  float w48;
+  load_window(S, window_rec(P, c, 0, lane), v, w48);
+  int done = 0;
+  for (int a = 0; a < 2 * NS; a++) {
+    if (done <= a) done = wait_progress(prog, a + 1);
+    emit_rows_t<NS>(P, S, c, duct_col, a, a >= NS ? obs_r : obs_b, env0, v, w48);
   }
 }
 
 // ---------------------------------------------------------------------------
 // phase L: load state columns
 // ---------------------------------------------------------------------------
+template <int AT = 0>
 __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, int lane, int env,
                                   bool valid) {
   const long long E = P.E;
-  for (int a = 0; a < P.A; a++) {
+  const int A = AT > 0 ? AT : P.A;
+#pragma unroll
+  for (int a = 0; a < (AT > 0 ? AT : A); a++) {
     size_t ai = (size_t)a * E + env;
     if (valid) {
       uint32_t p = S.pos[ai];
@@ -950,6 +1121,157 @@ __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, in
   }
 }
 
+// ---------------------------------------------------------------------------
+// phase M (combatant.py:459-489): action decode, move target, can_move_to and
+// the check_path feasibility, over (env, agent) pairs: pass p lane l handles
+// pair q = 64p + l of the workgroup (env q / A, agent q % A), so each pass
+// reads 64 consecutive action rows (one coalesced 1 KB load) and all passes'
+// loads of one batch are issued before any is used.
+// ---------------------------------------------------------------------------
+template <int DT, int MAXP>
+__device__ __forceinline__ void move_batch_t(const KParams &P, const KState &S, Cols &c, const void *actions,
+                             const uint8_t *row_kind, const uint32_t *mask, int env0, int nenv,
+                             int A, int p0, int np) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int npair = nenv * A;
+  f32x4 vf[DT == LNW_ACT_F32 ? MAXP : 1];
+  int4 vi[DT == LNW_ACT_I32 ? MAXP : 1];
+  double2 v01[DT == LNW_ACT_F64 ? MAXP : 1], v23[DT == LNW_ACT_F64 ? MAXP : 1];
+  int kd[DT == LNW_ACT_F64 ? MAXP : 1];
+#pragma unroll
+  for (int k = 0; k < MAXP; k++) {
+    if (k >= np) break;
+    int q = (p0 + k) * WAVE + lane;
+    q = q < npair ? q : 0;  // absent pairs re-read pair 0 (ignored)
+    const size_t row = ((size_t)env0 * A + q) * 4;
+    if constexpr (DT == LNW_ACT_F32) vf[k] = *(const f32x4 *)((const float *)actions + row);
+    else if constexpr (DT == LNW_ACT_I32) vi[k] = *(const int4 *)((const int32_t *)actions + row);
+    else {
+      const double2 *da = (const double2 *)((const double *)actions + row);
+      v01[k] = da[0];
+      v23[k] = da[1];
+      kd[k] = row_kind ? row_kind[(size_t)env0 * A + q] : K_F64;
+    }
+  }
+  uint32_t tg[MAXP];
+  int mw[MAXP];
+#pragma unroll
+  for (int k = 0; k < MAXP; k++) {
+    tg[k] = 0;
+    mw[k] = -1;
+    if (k >= np) break;
+    const int q = (p0 + k) * WAVE + lane;
+    const int e = q / A, a = q - (q / A) * A;
+    if (q >= npair || !c.alive0[a * PADB + e]) continue;
+    const uint32_t p = c.pos_old[a * PAD + e];
+    const int sx = pos_x(p), sy = pos_y(p);
+    const int t = c.type[a * PADB + e];
+    uint32_t target = p;  // no candidate
+    if constexpr (DT == LNW_ACT_I32) {
+      c.act0[a * PAD + e] = (double)vi[k].x;
+      c.act1[a * PAD + e] = (double)vi[k].y;
+      c.akind[a * PADB + e] = K_PYINT;
+      const int x = floordiv7(vi[k].z), y = pymod7(vi[k].z);
+      if (0 <= sx - 3 + x && sx - 3 + x < P.G && 0 <= sy - 3 + y && sy - 3 + y < P.G)
+        target = pack_pos(sx - 3 + x, sy - 3 + y) | 0x40000000u;
+    } else {
+      double a2, a3;
+      int kind;
+      if constexpr (DT == LNW_ACT_F32) {
+        c.act0[a * PAD + e] = vf[k].x;
+        c.act1[a * PAD + e] = vf[k].y;
+        a2 = vf[k].z;
+        a3 = vf[k].w;
+        kind = K_F32;
+      } else {
+        c.act0[a * PAD + e] = v01[k].x;
+        c.act1[a * PAD + e] = v01[k].y;
+        a2 = v23[k].x;
+        a3 = v23[k].y;
+        kind = kd[k];
+      }
+      c.akind[a * PADB + e] = (uint8_t)kind;
+      int nx, ny;
+      if (!move_target_dev(sx, sy, ship_speed(t), a2, a3, kind, nx, ny)) {
+        atomicOr(&S.err[env0 + e], (uint32_t)LNW_ERRF_NAN_ROUND);
+      } else if (0 <= nx && nx < 100 && 0 <= ny && ny < 100 &&
+                 !(cell_bits(mask, P.W16, nx, ny) & 1u)) {  // can_move_to (combatant.py:482-489)
+        target = pack_pos(nx, ny) | 0x40000000u;
+      }
+    }
+    tg[k] = target;
+    // check_path (combatant.py:382-408) from the move table when the target
+    // lies in its window (move_mode 0), else the A* below
+    if (target & 0x40000000u) {
+      const int tx = pos_x(target & 0x3fffffffu), ty = pos_y(target & 0x3fffffffu);
+      const int ox = tx - sx, oy = ty - sy;
+      if (P.move_mode == 0 && tx <= 99 && ty <= 99 && ox >= -R_MV && ox <= R_MV && oy >= -R_MV &&
+          oy <= R_MV) {
+        const int bit = (ox + R_MV) * MV_W + (oy + R_MV);
+        mw[k] = (int)(((size_t)(t == T_LS ? 1 : 0) * P.G * P.G + (size_t)sx * P.G + sy) * MV_WORDS +
+                      (bit >> 5)) * 32 + (bit & 31);
+      }
+    }
+  }
+  uint32_t w[MAXP];
+#pragma unroll
+  for (int k = 0; k < MAXP; k++) {
+    if (k >= np) break;
+    w[k] = S.mvtab[mw[k] >= 0 ? mw[k] >> 5 : 0];
+  }
+#pragma unroll
+  for (int k = 0; k < MAXP; k++) {
+    if (k >= np) break;
+    const int q = (p0 + k) * WAVE + lane;
+    const int e = q / A, a = q - (q / A) * A;
+    if (q >= npair || !(tg[k] & 0x40000000u)) continue;  // pos_new stays p (load_state)
+    if (mw[k] < 0) {  // outside the table: left flagged for the A* pass below
+      c.pos_new[a * PAD + e] = tg[k];
+      continue;
+    }
+    const bool feas = (w[k] >> (mw[k] & 31)) & 1u;
+    c.pos_new[a * PAD + e] = feas ? ((tg[k] & 0x3fffffffu) | 0x80000000u) : c.pos_old[a * PAD + e];
+  }
+}
+
+// check_path by A* for the candidates the table did not cover (still flagged
+// 0x40000000 in pos_new): one copy of the search for every action dtype.
+__device__ __forceinline__ void move_astar_pass(const KParams &P, const KState &S, Cols &c,
+                                                int nenv, int A) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int npair = nenv * A;
+#pragma unroll 1
+  for (int q = lane; q < npair; q += WAVE) {
+    const int e = q / A, a = q - (q / A) * A;
+    const uint32_t tgk = c.pos_new[a * PAD + e];
+    if (!(tgk & 0x40000000u)) continue;
+    const uint32_t p = c.pos_old[a * PAD + e];
+    const uint32_t t2 = tgk & 0x3fffffffu;
+    const bool feas = check_path_h(P, S, c.type[a * PADB + e], pos_x(p), pos_y(p), pos_x(t2),
+                                   pos_y(t2), c.open + lane, WAVE);
+    c.pos_new[a * PAD + e] = feas ? (t2 | 0x80000000u) : p;
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void move_phase(const KParams &P, const KState &S, Cols &c, const void *actions,
+                                  const uint8_t *row_kind, const uint32_t *mask, int env0,
+                                  int nenv, int A) {
+  // f32 (the rollout dtype) batches 8 passes; f64 / i32 go one pass at a time
+  constexpr int B = DT == LNW_ACT_F32 ? 8 : 1;
+  const int npass = (nenv * A + WAVE - 1) / WAVE;
+#pragma unroll 1
+  for (int p0 = 0; p0 < npass; p0 += B)
+    move_batch_t<DT, B>(P, S, c, actions, row_kind, mask, env0, nenv, A, p0,
+                        npass - p0 < B ? npass - p0 : B);
+}
+
+// diagnostics: per-workgroup phase timestamps (100 MHz real-time clock)
+__device__ inline void prof_stamp(const KState &S, int slot) {
+  if (S.prof && (threadIdx.x & (WAVE - 1)) == 0)
+    S.prof[(size_t)blockIdx.x * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 
 // ---------------------------------------------------------------------------
@@ -957,12 +1279,14 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // ---------------------------------------------------------------------------
 // NB/NR > 0: compile-time ship counts (register pair loop in get_obs, unrolled
 // observation copy-out); NB = NR = 0: runtime counts from P.
+// NB/NR > 0 run two waves per workgroup: wave 0 steps the envs, wave 1 emits
+// the observation rows (emit_wave_t).
 template <int NB, int NR>
-__global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *actions,
-                                                  const uint8_t *row_kind, float *obs_b,
-                                                  float *obs_r, float *rew_b, float *rew_r,
-                                                  int32_t *done_out, float *cog_out) {
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step_kernel(
+    KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
+    float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = threadIdx.x / WAVE;
   const int env0 = blockIdx.x * EPW;
   const int env = env0 + lane;
   const long long E = P.E;
@@ -974,81 +1298,49 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
   LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
+  __shared__ int prog;
+  // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
+  // table mode; the terrain mask LDS is then reused as the emission stage, so
+  // the rare out-of-table LOS march reads the global copy
+  const bool emit = ST && P.los_mode == 0 && nenv == WAVE && !(P.dbg_skip & 3);
+  if (wid == 1) {
+    __syncthreads();
+    if constexpr (ST) {
+      if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
+    }
+    prof_stamp(S, 5);
+    return;
+  }
+  prof_stamp(S, 0);
 
   for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
   const uint32_t *mask = c.mask;
-  load_state(P, S, c, lane, env, valid);
+  load_state<NB + NR>(P, S, c, lane, env, valid);
   double duct = valid ? S.duct[env] : 1.0;
   duct_col[lane] = duct;
+  if (lane == 0) prog = -1;
   __syncthreads();
 
   // ---- phase M: movement feasibility for every agent of this env --------
   // M1: load each action row once (a0/a1 kept in LDS for phase S) and compute
   //     the move target; M2: feasibility lookups (independent across agents).
   const int dt = P.act_dtype;
-  if (valid && !(P.dbg_skip & 4)) {
-    for (int a = 0; a < A; a++) {
-      if (!COLB(c.alive0, a)) continue;
-      uint32_t p = COLW(c.pos_old, a);
-      int sx = pos_x(p), sy = pos_y(p);
-      int t = COLB(c.type, a);
-      size_t row = ((size_t)env * A + a) * 4;
-      uint32_t target = p;  // no candidate
-      if (dt == LNW_ACT_I32) {
-        int4 v = *(const int4 *)((const int32_t *)actions + row);
-        COLW(c.act0, a) = (double)v.x;
-        COLW(c.act1, a) = (double)v.y;
-        COLB(c.akind, a) = K_PYINT;
-        int x = floordiv7(v.z), y = pymod7(v.z);
-        if (0 <= sx - 3 + x && sx - 3 + x < P.G && 0 <= sy - 3 + y && sy - 3 + y < P.G)
-          target = pack_pos(sx - 3 + x, sy - 3 + y) | 0x40000000u;
-      } else {
-        double a2, a3;
-        int kind;
-        if (dt == LNW_ACT_F32) {
-          f32x4 v = *(const f32x4 *)((const float *)actions + row);
-          COLW(c.act0, a) = v.x;
-          COLW(c.act1, a) = v.y;
-          a2 = v.z;
-          a3 = v.w;
-          kind = K_F32;
-        } else {
-          const double2 *da = (const double2 *)((const double *)actions + row);
-          double2 v01 = da[0], v23 = da[1];
-          COLW(c.act0, a) = v01.x;
-          COLW(c.act1, a) = v01.y;
-          a2 = v23.x;
-          a3 = v23.y;
-          kind = row_kind ? row_kind[(size_t)env * A + a] : K_F64;
-        }
-        COLB(c.akind, a) = (uint8_t)kind;
-        int nx, ny;
-        bool ok = move_target_dev(sx, sy, ship_speed(t), a2, a3, kind, nx, ny);
-        if (!ok) {
-          S.err[env] |= LNW_ERRF_NAN_ROUND;
-        } else if (0 <= nx && nx < 100 && 0 <= ny && ny < 100 &&
-                   !(cell_bits(mask, P.W16, nx, ny) & 1u)) {  // can_move_to (combatant.py:482-489)
-          target = pack_pos(nx, ny) | 0x40000000u;
-        }
-      }
-      COLW(c.pos_new, a) = target;
-    }
-    for (int a = 0; a < A; a++) {
-      uint32_t tg = COLW(c.pos_new, a);
-      if (!(tg & 0x40000000u)) continue;
-      uint32_t p = COLW(c.pos_old, a);
-      const uint32_t t2 = tg & 0x3fffffffu;
-      bool feas = check_path_h(P, S, COLB(c.type, a), pos_x(p), pos_y(p), pos_x(t2), pos_y(t2),
-                               c.open + lane, WAVE);
-      COLW(c.pos_new, a) = feas ? ((tg & 0x3fffffffu) | 0x80000000u) : p;
-    }
+  if (!(P.dbg_skip & 4)) {
+    if (dt == LNW_ACT_F32) move_phase<LNW_ACT_F32>(P, S, c, actions, row_kind, mask, env0, nenv, A);
+    else if (dt == LNW_ACT_F64) move_phase<LNW_ACT_F64>(P, S, c, actions, row_kind, mask, env0, nenv, A);
+    else move_phase<LNW_ACT_I32>(P, S, c, actions, row_kind, mask, env0, nenv, A);
+    move_astar_pass(P, S, c, nenv, A);
+    wave_lds_sync();
   }
 
   // ---- phase S: sequential agent loop ------------------------------------
   int done = 1;
   float cog = NAN;
+  prof_stamp(S, 1);
   if (valid && !(P.dbg_skip & 2)) {
-    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E, max_range2(P, duct)};
+    if (emit) publish_progress(&prog, 0);
+    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), emit ? S.mask2 : mask, E,
+          max_range2(P, duct)};
     Neut N{{0, 0}, {0u, 0u}};
     int ev[8];
 #pragma unroll
@@ -1057,7 +1349,8 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
     double bsx = 0, bsy = 0, rsx = 0, rsy = 0;
     int nbp = 0, nrp = 0;
     for (int a = 0; a < A; a++) {
-      if (!COLB(c.alive0, a)) { COLW(c.reward, a) = 0.0; continue; }
+     do {
+      if (!COLB(c.alive0, a)) { COLW(c.reward, a) = 0.0; break; }
       const int side = a >= nb;
       uint32_t p0 = COLW(c.pos_cur, a);
       if (!side) {
@@ -1121,6 +1414,8 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
         if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
       }
       hits[side] += destroyed;
+     } while (0);
+      if (emit) publish_progress(&prog, a + 1);
     }
     // ---- tail (game.py:409-520) -------------------------------------------
     int nbl = ev[0] - N.cnt[0];
@@ -1197,6 +1492,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
       if (rew_r) rew_r[(size_t)env * nr + a] = (float)COLW(c.reward, nb + a);
     if (done_out) done_out[env] = done;
     if (cog_out) cog_out[env] = cog;
+    prof_stamp(S, 2);
     // ---- phase W: store state (alive updated by the neutralized lists) --
     bool do_reset = P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
     for (int a = 0; a < A; a++) {
@@ -1217,9 +1513,10 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
     S.rng[env] = X.rng.ctr;
     if (X.rng.err) S.err[env] |= X.rng.err;
   }
+  prof_stamp(S, 3);
+  if ((P.dbg_skip & 1) || emit) return;
   __syncthreads();
   // ---- phase O: observations ---------------------------------------------
-  if (P.dbg_skip & 1) return;
   if constexpr (ST) write_obs_t<NB, NR>(P, S, c, duct_col, obs_b, obs_r, env0, nenv);
   else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
 }
@@ -1229,7 +1526,7 @@ __global__ __launch_bounds__(64) void step_kernel(KParams P, KState S, void *act
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
                                                      float *obs_r) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
   const int env0 = blockIdx.x * EPW;
   const int env = env0 + lane;
   const long long E = P.E;
@@ -1483,6 +1780,7 @@ struct lnw_handle {
   // device buffers
   uint8_t *d_grid = nullptr;
   float *d_gridf = nullptr, *d_winf = nullptr, *d_dummy = nullptr;
+  unsigned long long *d_prof = nullptr;  // LNW_PROF phase timestamps
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -1517,7 +1815,7 @@ KState make_state(lnw_handle *h) {
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
   s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
-  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
   s.sp_pos_env = nullptr;
@@ -1531,6 +1829,32 @@ size_t step_lds_bytes(const lnw_handle *h) {
 }
 
 }  // namespace
+
+// LNW_PROF diagnostics: mean per-workgroup phase spans and the grid-wide
+// start / end spread of one step launch (synchronises the stream).
+void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
+  std::vector<unsigned long long> t((size_t)nwg * 8);
+  if (hipMemcpyAsync(t.data(), h->d_prof, t.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return;
+  double sM = 0, sS = 0, sW = 0, s1 = 0;
+  unsigned long long t0 = ~0ull, tend0 = 0, tend1 = 0;
+  int n1 = 0;
+  for (int w = 0; w < nwg; w++) {
+    const unsigned long long *r = &t[(size_t)w * 8];
+    sM += (double)(r[1] - r[0]);
+    sS += (double)(r[2] - r[1]);
+    sW += (double)(r[3] - r[2]);
+    if (r[5]) { s1 += (double)(r[5] - r[0]); n1++; if (r[5] > tend1) tend1 = r[5]; }
+    if (r[0] < t0) t0 = r[0];
+    if (r[3] > tend0) tend0 = r[3];
+  }
+  const double us = 0.01;  // 100 MHz ticks
+  fprintf(stderr, "[lnw prof] wg=%d mean L+M %.2f us, S %.2f us, W %.2f us, wave1 end-from-start %.2f us; "
+                  "grid: last wave0 end %.2f us, last wave1 end %.2f us after first start\n",
+          nwg, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
+          (double)(tend0 - t0) * us, tend1 ? (double)(tend1 - t0) * us : 0.0);
+}
 
 extern "C" {
 
@@ -1610,6 +1934,7 @@ int lnw_destroy(lnw_handle *h) {
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   for (void *p : h->allocs) (void)hipFree(p);
+  if (h->d_prof) (void)hipFree(h->d_prof);
   delete h;
   return 0;
 }
@@ -1749,9 +2074,14 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
+  if (getenv("LNW_PROF")) {
+    if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(h->d_prof, 0, (size_t)grid.x * 8 * sizeof(unsigned long long), st));
+    s.prof = h->d_prof;
+  }
   bool generic = getenv("LNW_FORCE_GENERIC") != nullptr;
 #define LNW_STEP(NB_, NR_)                                                                       \
-  step_kernel<NB_, NR_><<<grid, block, lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
+  step_kernel<NB_, NR_><<<grid, dim3(NB_ > 0 ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
                                                  done_dev, cog_dev)
   if (!generic && h->nb == 4 && h->nr == 4) LNW_STEP(4, 4);
@@ -1760,6 +2090,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else LNW_STEP(0, 0);
 #undef LNW_STEP
   HIPCHK(hipGetLastError());
+  if (s.prof) prof_report(h, st, (int)grid.x);
   return 0;
 }
 
