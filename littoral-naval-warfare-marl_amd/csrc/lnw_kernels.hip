@@ -1267,9 +1267,15 @@ __device__ __forceinline__ void move_phase(const KParams &P, const KState &S, Co
 }
 
 // diagnostics: per-workgroup phase timestamps (100 MHz real-time clock)
+__device__ inline unsigned long long prof_now(const KState &S) {
+  return S.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+}
+__device__ inline void prof_put(const KState &S, int slot, unsigned long long v) {
+  if (S.prof && (threadIdx.x & (WAVE - 1)) == 0) S.prof[(size_t)blockIdx.x * 16 + slot] = v;
+}
 __device__ inline void prof_stamp(const KState &S, int slot) {
   if (S.prof && (threadIdx.x & (WAVE - 1)) == 0)
-    S.prof[(size_t)blockIdx.x * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+    S.prof[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
@@ -1320,6 +1326,7 @@ __global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step
   duct_col[lane] = duct;
   if (lane == 0) prog = -1;
   __syncthreads();
+  prof_stamp(S, 4);
 
   // ---- phase M: movement feasibility for every agent of this env --------
   // M1: load each action row once (a0/a1 kept in LDS for phase S) and compute
@@ -1348,7 +1355,9 @@ __global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step
     int hits[2] = {0, 0};
     double bsx = 0, bsy = 0, rsx = 0, rsy = 0;
     int nbp = 0, nrp = 0;
+    unsigned long long pf_fire = 0, pf_obs = 0, pf_rest = 0;
     for (int a = 0; a < A; a++) {
+      unsigned long long pt0 = prof_now(S), pt1 = pt0, pt2 = pt0;
      do {
       if (!COLB(c.alive0, a)) { COLW(c.reward, a) = 0.0; break; }
       const int side = a >= nb;
@@ -1391,6 +1400,7 @@ __global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step
           if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
         }
       }
+      pt1 = prof_now(S);
       if (side) ev[6] += destroyed; else ev[5] += destroyed;
       if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
       else {
@@ -1406,6 +1416,7 @@ __global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step
       } else {
         get_obs_dev(X, a);
       }
+      pt2 = prof_now(S);
       double r = reward_dev(X, a, moved, engage, destroyed);
       COLW(c.reward, a) = r;
       if (!side) {
@@ -1416,7 +1427,12 @@ __global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step
       hits[side] += destroyed;
      } while (0);
       if (emit) publish_progress(&prog, a + 1);
+      const unsigned long long pt3 = prof_now(S);
+      pf_fire += pt1 - pt0; pf_obs += pt2 - pt1; pf_rest += pt3 - pt2;
     }
+    prof_put(S, 8, pf_fire);
+    prof_put(S, 9, pf_obs);
+    prof_put(S, 10, pf_rest);
     // ---- tail (game.py:409-520) -------------------------------------------
     int nbl = ev[0] - N.cnt[0];
     int nrl = ev[1] - N.cnt[1];
@@ -1781,6 +1797,9 @@ struct lnw_handle {
   uint8_t *d_grid = nullptr;
   float *d_gridf = nullptr, *d_winf = nullptr, *d_dummy = nullptr;
   unsigned long long *d_prof = nullptr;  // LNW_PROF phase timestamps
+  // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
+  int dbg_skip = 0;
+  bool prof = false, force_generic = false;
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -1833,26 +1852,35 @@ size_t step_lds_bytes(const lnw_handle *h) {
 // LNW_PROF diagnostics: mean per-workgroup phase spans and the grid-wide
 // start / end spread of one step launch (synchronises the stream).
 void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
-  std::vector<unsigned long long> t((size_t)nwg * 8);
+  std::vector<unsigned long long> t((size_t)nwg * 16);
   if (hipMemcpyAsync(t.data(), h->d_prof, t.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return;
-  double sM = 0, sS = 0, sW = 0, s1 = 0;
+  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0;
   unsigned long long t0 = ~0ull, tend0 = 0, tend1 = 0;
   int n1 = 0;
   for (int w = 0; w < nwg; w++) {
-    const unsigned long long *r = &t[(size_t)w * 8];
-    sM += (double)(r[1] - r[0]);
+    const unsigned long long *r = &t[(size_t)w * 16];
+    sL += (double)(r[4] - r[0]);
+    sM += (double)(r[1] - r[4]);
     sS += (double)(r[2] - r[1]);
     sW += (double)(r[3] - r[2]);
     if (r[5]) { s1 += (double)(r[5] - r[0]); n1++; if (r[5] > tend1) tend1 = r[5]; }
     if (r[0] < t0) t0 = r[0];
     if (r[3] > tend0) tend0 = r[3];
   }
+  double sf = 0, so = 0, sr = 0;
+  for (int w = 0; w < nwg; w++) {
+    sf += (double)t[(size_t)w * 16 + 8];
+    so += (double)t[(size_t)w * 16 + 9];
+    sr += (double)t[(size_t)w * 16 + 10];
+  }
   const double us = 0.01;  // 100 MHz ticks
-  fprintf(stderr, "[lnw prof] wg=%d mean L+M %.2f us, S %.2f us, W %.2f us, wave1 end-from-start %.2f us; "
+  fprintf(stderr, "[lnw prof] S split: engage %.2f us, get_obs %.2f us, reward+rest %.2f us\n",
+          sf / nwg * us, so / nwg * us, sr / nwg * us);
+  fprintf(stderr, "[lnw prof] wg=%d mean L %.2f us, M %.2f us, S %.2f us, W %.2f us, wave1 end-from-start %.2f us; "
                   "grid: last wave0 end %.2f us, last wave1 end %.2f us after first start\n",
-          nwg, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
+          nwg, sL / nwg * us, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
           (double)(tend0 - t0) * us, tend1 ? (double)(tend1 - t0) * us : 0.0);
 }
 
@@ -1881,6 +1909,9 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   HIPCHK(hipSetDevice(device));
   lnw_handle *h = new lnw_handle();
   h->device = device;
+  if (const char *dbg = getenv("LNW_DEBUG_SKIP")) h->dbg_skip = atoi(dbg);
+  h->prof = getenv("LNW_PROF") != nullptr;
+  h->force_generic = getenv("LNW_FORCE_GENERIC") != nullptr;
   h->params = *params;
   h->E = n_envs; h->nb = nb; h->nr = nr; h->A = nb + nr;
   h->nmax = nb > nr ? nb : nr;
@@ -2069,17 +2100,17 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
     return fail(LNW_EINVAL, "integer actions go with DISCRETE mode and only with it");
   KParams k = h->kp;
   k.act_dtype = action_dtype;
-  if (const char *dbg = getenv("LNW_DEBUG_SKIP")) k.dbg_skip = atoi(dbg);
+  k.dbg_skip = h->dbg_skip;
   KState s = make_state(h);
   size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
-  if (getenv("LNW_PROF")) {
-    if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * 8 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(h->d_prof, 0, (size_t)grid.x * 8 * sizeof(unsigned long long), st));
+  if (h->prof) {
+    if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(h->d_prof, 0, (size_t)grid.x * 16 * sizeof(unsigned long long), st));
     s.prof = h->d_prof;
   }
-  bool generic = getenv("LNW_FORCE_GENERIC") != nullptr;
+  bool generic = h->force_generic;
 #define LNW_STEP(NB_, NR_)                                                                       \
   step_kernel<NB_, NR_><<<grid, dim3(NB_ > 0 ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \

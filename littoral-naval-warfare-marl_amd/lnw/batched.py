@@ -89,6 +89,14 @@ class BatchedGame:
         self.done = torch.ones((self.E,), dtype=torch.int32, device=dev)
         self.cog = torch.zeros((self.E,), dtype=torch.float32, device=dev)
         self._spawn = None
+        # step() hot path: output pointers and the accepted action layout, cached
+        self._outp = tuple(_ptr(t) for t in (self.obs_blue, self.obs_red, self.rew_blue,
+                                             self.rew_red, self.done, self.cog))
+        self._outd = dict(obs_blue=self.obs_blue, obs_red=self.obs_red, rew_blue=self.rew_blue,
+                          rew_red=self.rew_red, done=self.done, cog=self.cog)
+        self._ashape = torch.Size((self.E, self.A, 4))
+        self._dtypes = {torch.float32: LNW_ACT_F32, torch.float64: LNW_ACT_F64,
+                        torch.int32: LNW_ACT_I32}
 
     # ---------------------------------------------------------------- rng
     def set_rng(self, seed):
@@ -144,23 +152,18 @@ class BatchedGame:
         (continuous) or int32 (discrete). Mutated in place where the reference
         mutates its action rows (game.py:379). Returns the output tensors."""
         a = actions
-        assert a.is_cuda and a.is_contiguous() and tuple(a.shape) == (self.E, self.A, 4)
-        if a.dtype == torch.float32:
-            dt = LNW_ACT_F32
-        elif a.dtype == torch.float64:
-            dt = LNW_ACT_F64
-        elif a.dtype == torch.int32:
-            dt = LNW_ACT_I32
-        else:
+        if a.shape != self._ashape or not a.is_cuda or not a.is_contiguous():
+            raise ValueError(f"actions must be a contiguous cuda tensor of shape {tuple(self._ashape)}")
+        dt = self._dtypes.get(a.dtype)
+        if dt is None:
             raise TypeError(f"unsupported action dtype {a.dtype}")
         rk = None
         if row_kind is not None:
-            rk = torch.as_tensor(row_kind, dtype=torch.uint8, device=self.device).contiguous()
-        check(self.L.lnw_step(self.h, _ptr(a), dt, _ptr(rk), _ptr(self.obs_blue),
-                              _ptr(self.obs_red), _ptr(self.rew_blue), _ptr(self.rew_red),
-                              _ptr(self.done), _ptr(self.cog), self._stream()))
-        return dict(obs_blue=self.obs_blue, obs_red=self.obs_red, rew_blue=self.rew_blue,
-                    rew_red=self.rew_red, done=self.done, cog=self.cog)
+            rk = _ptr(torch.as_tensor(row_kind, dtype=torch.uint8, device=self.device).contiguous())
+        ob, orr, rb, rr, dn, cg = self._outp
+        check(self.L.lnw_step(self.h, a.data_ptr(), dt, rk, ob, orr, rb, rr, dn, cg,
+                              torch.cuda.current_stream(self.device).cuda_stream))
+        return self._outd
 
     def observe(self, agent=-1):
         """ship.get_obs() for every live ship (agent=-1, blue then red), one side
