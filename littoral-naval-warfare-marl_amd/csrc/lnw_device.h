@@ -243,13 +243,32 @@ __device__ inline double ship_rcs(int t) { return t == T_SMALL ? 0.7 : (t == T_L
 __device__ inline int missiles0(int t) { return t == T_LS ? 0 : (t == T_SMALL ? 4 : 8); }
 __device__ inline double miss_norm(int t) { return t == T_SMALL ? 4.0 : 8.0; }
 
+// Small parameter tables indexed by per-lane values: selects between the
+// (wave-uniform, scalar-loaded) entries instead of per-lane loads from the
+// kernel-argument segment.
+__device__ inline double d5_sel(const KParams &P, int mi, int mj) {
+  const double r0 = mj ? P.d5[0][1] : P.d5[0][0];
+  const double r1 = mj ? P.d5[1][1] : P.d5[1][0];
+  return mi ? r1 : r0;
+}
+template <class TAB>
+__device__ inline auto hit_sel(const TAB &tab, int hp, int n) -> decltype(tab[0][0] + 0) {
+  auto row = [&](int h) {
+    auto v = tab[h][0];
+#pragma unroll
+    for (int k = 1; k < 9; k++) v = n == k ? tab[h][k] : v;
+    return v;
+  };
+  return hp ? row(1) : row(0);
+}
+
 // radar_range / ew_range (combatant.py:235-247) -> squared integer ranges
 __device__ inline int radar_r(const KParams &P, double duct, int ti, int tj) {
-  double d = P.d5[mast_cls(ti)][mast_cls(tj)];
+  double d = d5_sel(P, mast_cls(ti), mast_cls(tj));
   return (int)ceil(d * ship_rcs(tj) * duct);
 }
 __device__ inline int ew_r(const KParams &P, double duct, int ti, int tj) {
-  double d = P.d5[mast_cls(ti)][mast_cls(tj)] * duct;
+  double d = d5_sel(P, mast_cls(ti), mast_cls(tj)) * duct;
   d = 2.0 * d;
   return (int)ceil(d);
 }

@@ -61,7 +61,12 @@ __host__ __device__ constexpr int stage_stride(int ns) {
   return (((4 * ns + 52) / 4) & 1) ? (4 * ns + 52) : (4 * ns + 56);
 }
 // Phase-O LDS: staged rows (one pass = the rows of WAVE/A envs) | x/G LUT.
-__host__ __device__ inline int envs_per_pass(int A) { return WAVE / A; }
+// (half a wave's worth of rows when a workgroup holds half a wave of envs, to
+// keep its LDS within an eighth of the CU's)
+constexpr int OBS_PASS_DIV = EPW == WAVE ? 1 : 2;
+__host__ __device__ constexpr int envs_per_pass(int A) {
+  return WAVE / A / OBS_PASS_DIV > 0 ? WAVE / A / OBS_PASS_DIV : 1;
+}
 __host__ __device__ inline int stage_rows_bytes(int A, int nb, int nr) {
   int epg = envs_per_pass(A);
   return epg * (nb * stage_stride(nb) + nr * stage_stride(nr)) * 4;
@@ -98,7 +103,7 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   // the A* open lists (phase M) alias the rewards (first written in phase S)
   L.reward = o;
   L.open = o;
-  o += (A * PAD * 8 > OPEN_CAP * WAVE * 4) ? A * PAD * 8 : OPEN_CAP * WAVE * 4;
+  o += (A * PAD * 8 > OPEN_CAP * EPW * 4) ? A * PAD * 8 : OPEN_CAP * EPW * 4;
   L.act0 = o; o += A * PAD * 8;
   L.act1 = o; o += A * PAD * 8;
   L.observed = o; o += nmax * PAD * 4;
@@ -112,7 +117,9 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   o = (o + 15) & ~15;
   L.mask = o;
   L.estage = o;
-  o += mask_words * 4 > estage_bytes(G) ? mask_words * 4 : estage_bytes(G);
+  // the emission stage exists only with full-wave workgroups (two-wave kernels)
+  const int est = EPW == WAVE ? estage_bytes(G) : 0;
+  o += mask_words * 4 > est ? mask_words * 4 : est;
   L.total = o;
   return L;
 }
@@ -498,7 +505,7 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
     if (miss == 0) return false;
     int mk = COLB(c.mkind, a);
     double u1 = X.rng.uniform();
-    bool detected = !(u1 < P.det_q[COLW(c.radar_cur, t) == 1 ? 0 : 1]);
+    bool detected = !(u1 < (COLW(c.radar_cur, t) == 1 ? P.det_q[0] : P.det_q[1]));
     int hp = detected ? 0 : 1;
     double num;
     int kn;
@@ -522,9 +529,9 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
     double u2 = X.rng.uniform();
     if (n < 0 || n > 8) { X.rng.err |= LNW_ERRF_MISSILES; n = n < 0 ? 0 : 8; }
     if (kn == K_F32)
-      hit = (float)u2 < P.hit32[hp][n];
+      hit = (float)u2 < hit_sel(P.hit32, hp, n);
     else
-      hit = u2 < P.hit64[hp][n];
+      hit = u2 < hit_sel(P.hit64, hp, n);
   }
   if (hit) {
     int ts = t >= P.nb;
@@ -564,7 +571,7 @@ __device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int 
   if (red && P.aggressive && t != T_LS) {
     int dx = x - 15, dy = y - 60;
     double nom = fmax(sqrt((double)(dx * dx + dy * dy)), 1.0);
-    double d = (1.0 / (nom / P.den[mast_cls(t)])) * 1.0;
+    double d = (1.0 / (nom / (mast_cls(t) ? P.den[1] : P.den[0]))) * 1.0;
     r += d;
   }
   if (t == T_LS) {
@@ -892,7 +899,7 @@ template <int NB, int NR>
 __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, Cols &c, const double *duct_col,
                             float *obs_b, float *obs_r, int env0, int nenv) {
   static_assert(NB == NR, "templated obs rows assume equal team sizes");
-  constexpr int A = NB + NR, EPG = WAVE / A;
+  constexpr int A = NB + NR, EPG = envs_per_pass(NB + NR);
   const int lane = threadIdx.x & (WAVE - 1);
   const int my_e = lane / A, my_k = lane - (lane / A) * A;
   const int side = my_k >= NB;
@@ -1240,15 +1247,16 @@ __device__ __forceinline__ void move_astar_pass(const KParams &P, const KState &
                                                 int nenv, int A) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int npair = nenv * A;
+  if (lane >= EPW) return;  // open lists exist for EPW lanes
 #pragma unroll 1
-  for (int q = lane; q < npair; q += WAVE) {
+  for (int q = lane; q < npair; q += EPW) {
     const int e = q / A, a = q - (q / A) * A;
     const uint32_t tgk = c.pos_new[a * PAD + e];
     if (!(tgk & 0x40000000u)) continue;
     const uint32_t p = c.pos_old[a * PAD + e];
     const uint32_t t2 = tgk & 0x3fffffffu;
     const bool feas = check_path_h(P, S, c.type[a * PADB + e], pos_x(p), pos_y(p), pos_x(t2),
-                                   pos_y(t2), c.open + lane, WAVE);
+                                   pos_y(t2), c.open + lane, EPW);
     c.pos_new[a * PAD + e] = feas ? (t2 | 0x80000000u) : p;
   }
 }
@@ -1288,7 +1296,7 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // NB/NR > 0 run two waves per workgroup: wave 0 steps the envs, wave 1 emits
 // the observation rows (emit_wave_t).
 template <int NB, int NR>
-__global__ __launch_bounds__(NB > 0 ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step_kernel(
+__global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -2112,7 +2120,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   }
   bool generic = h->force_generic;
 #define LNW_STEP(NB_, NR_)                                                                       \
-  step_kernel<NB_, NR_><<<grid, dim3(NB_ > 0 ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
+  step_kernel<NB_, NR_><<<grid, dim3(NB_ > 0 && EPW == WAVE ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
                                                  done_dev, cog_dev)
   if (!generic && h->nb == 4 && h->nr == 4) LNW_STEP(4, 4);
