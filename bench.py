@@ -30,6 +30,12 @@ REF_RED = [(98, 48), (98, 52), (98, 56), (96, 52)]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+# 8 small blue vs 8 large + 2 LandingShip red, landing
+# ops, the 200x200 grid, spawns on water cells of a box inside x in [0, 99]
+CONFIG4 = dict(blue=["small"] * 8, red=["large"] * 8 + ["ls"] * 2, G=200, landing_ops=True,
+               box=((20, 60), (80, 140)), rand_ls=[0] * 16 + [1, 1], envs=8192)
+
+
 def algorithmic_bytes(nb, nr):
     """Minimum HBM bytes one env-step must move:
     actions in (f32), observations + rewards + done + cog out, and the SoA state
@@ -53,6 +59,8 @@ def parse():
     p.add_argument("--move-mode", type=int, default=0, help="0 move table, 1 direct A*")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                   help="threads for the CPU baseline (the GPU box's share is 16 cores)")
     p.add_argument("--secondary", action="store_true",
                    help="also time melee spawns and the march/A* variants (stderr + JSON)")
     return p.parse_args()
@@ -62,22 +70,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_game(E, rank, args, spawns, los_mode, move_mode):
-    from lnw.batched import BatchedGame
+def make_game(E, rank, args, spawns, los_mode, move_mode, cfg=None):
+    from lnw.batched import BatchedGame, default_grid
     from lnw.config import Scenario
-    sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=True,
-                  auto_reset=True, episode_steps=40, los_mode=los_mode, move_mode=move_mode)
-    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, device=torch.cuda.current_device(),
-                    env_id_base=rank * E, seed=1234)
-    box = ((40, 40), (57, 65)) if spawns == "melee" else None
-    g.reset(positions=REF_BLUE + REF_RED, box=box)
+    if cfg is None:
+        sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=True,
+                      auto_reset=True, episode_steps=40, los_mode=los_mode, move_mode=move_mode)
+        g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc,
+                        device=torch.cuda.current_device(), env_id_base=rank * E, seed=1234)
+        box = ((40, 40), (57, 65)) if spawns == "melee" else None
+        g.reset(positions=REF_BLUE + REF_RED, box=box)
+        return g
+    sc = Scenario(landing_ops=cfg["landing_ops"], tactics="aggressive", side="blue",
+                  trained_red=True, auto_reset=True, episode_steps=40, los_mode=los_mode,
+                  move_mode=move_mode)
+    g = BatchedGame(E, cfg["blue"], cfg["red"], scenario=sc, device=torch.cuda.current_device(),
+                    env_id_base=rank * E, seed=1234, grid=default_grid(cfg["G"]))
+    n = len(cfg["blue"]) + len(cfg["red"])
+    g.reset(positions=[(0, 0)] * n, rand_ls=cfg["rand_ls"], box=cfg["box"])
     return g
 
 
-def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmup):
+def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmup, cfg=None):
     from lnw import _abi
     L = _abi.load()
-    g = make_game(E, rank, args, spawns, los_mode, move_mode)
+    g = make_game(E, rank, args, spawns, los_mode, move_mode, cfg)
     A = g.A
     # inputs resident before the timed region: actions for every step
     acts = torch.empty((warmup + steps, E, A, 4), dtype=torch.float32, device="cuda")
@@ -114,35 +131,85 @@ def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmu
     return elapsed, kms, err, episodes
 
 
-def cpu_baseline(seconds):
+def ray_march(n=1 << 22, reps=10):
+    """The LOS ray-march kernel alone (lnw_los_batch, combatant.py:436-456) on
+    n random rays with offsets in [-37, 37]^2 (the sensor ranges): rays/s and
+    reference-equivalent Bresenham cells/s (max(|dx|,|dy|) + 1 per ray)."""
+    from lnw import _abi
+    from lnw.batched import default_grid
+    L = _abi.load()
+    rng = np.random.default_rng(3)
+    x1 = rng.integers(0, 100, n)
+    y1 = rng.integers(0, 100, n)
+    x2 = np.clip(x1 + rng.integers(-37, 38, n), 0, 99)
+    y2 = np.clip(y1 + rng.integers(-37, 38, n), 0, 99)
+    cells = float(np.sum(np.maximum(np.abs(x2 - x1), np.abs(y2 - y1)) + 1))
+    pairs = torch.from_numpy(np.stack([x1, y1, x2, y2], 1).astype(np.int16)).cuda()
+    grid = torch.from_numpy(default_grid(100)).cuda()
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def launch():
+        _abi.check(L.lnw_los_batch(ctypes.c_void_p(grid.data_ptr()), 100,
+                                   ctypes.c_void_p(pairs.data_ptr()), n, 74, 70,
+                                   ctypes.c_void_p(out.data_ptr()), stream))
+    launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) / reps * 1e-3
+    return dict(rays_per_sec=n / sec, cells_per_sec=cells / sec, ms_per_launch=sec * 1e3,
+                rays=n, mean_cells_per_ray=cells / n)
+
+
+def cpu_baseline(seconds, threads):
     """The CPU oracle (oracle/lnw_oracle.c, a C restatement of the reference
-    step) timed on one host core over a bounded sample of the same workload."""
+    step) timed on the host over a bounded sample of the same workload: one
+    thread, then `threads` threads over disjoint env ranges (ctypes drops the
+    GIL). The threaded rate is the reported baseline."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle
+    from concurrent.futures import ThreadPoolExecutor
     L = _oracle.lib()
-    L.orc_bench.restype = ctypes.c_int64
-    L.orc_bench.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                            ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+    L.orc_bench_range.restype = ctypes.c_int64
+    L.orc_bench_range.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
     from lnw.batched import default_grid
     grid = np.ascontiguousarray(default_grid(100), np.uint8)
     P = _oracle.OrcParams(0, 0, 1, 1, 1, 0.4, 74, 70, 14, 82)
     types = np.array([0] * 4 + [1] * 4, np.int32)
     pos = np.array(REF_BLUE + REF_RED, np.int32).reshape(-1)
 
-    def run(n_envs, n_steps):
-        t = time.perf_counter()
-        n = L.orc_bench(ctypes.byref(P), grid.ctypes.data_as(ctypes.c_void_p), 100, 4, 4,
-                        types.ctypes.data_as(ctypes.c_void_p), pos.ctypes.data_as(ctypes.c_void_p),
-                        n_envs, n_steps, 40, 42)
-        return n, time.perf_counter() - t
+    def run(env0, n_envs):
+        return L.orc_bench_range(ctypes.byref(P), grid.ctypes.data_as(ctypes.c_void_p), 100, 4, 4,
+                                 types.ctypes.data_as(ctypes.c_void_p),
+                                 pos.ctypes.data_as(ctypes.c_void_p), env0, n_envs, 40, 40, 42)
 
-    n, dt = run(16, 40)
-    envs = max(16, int(16 * seconds / max(dt, 1e-3)))
-    n, dt = run(envs, 40)
-    return dict(value=n / dt, unit="env-steps/sec", cores=1, kind="port",
-                sample=f"{envs} envs x 40 steps (4v4, reference spawns, U[0,1) f32 actions, "
-                       f"auto-reset), CPU oracle restatement single-threaded, {dt:.1f} s")
+    t = time.perf_counter()
+    run(0, 16)
+    dt = time.perf_counter() - t
+    per_env = max(dt / 16, 1e-5)
+    half = seconds / 2
+    env1 = max(16, int(half / per_env))
+    t = time.perf_counter()
+    n1 = run(0, env1)
+    dt1 = time.perf_counter() - t
+    envs_t = max(16, int(half / per_env)) * threads
+    chunk = (envs_t + threads - 1) // threads
+    t = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        nt = sum(ex.map(lambda i: run(i * chunk, chunk), range(threads)))
+    dtt = time.perf_counter() - t
+    return dict(value=nt / dtt, unit="env-steps/sec", cores=threads, kind="port",
+                sample=f"{threads * chunk} envs x 40 steps on {threads} threads ({dtt:.1f} s); "
+                       f"1 thread: {env1} envs x 40 steps ({dt1:.1f} s); 4v4, reference spawns, "
+                       "U[0,1) f32 actions, auto-reset; CPU oracle restatement",
+                single_thread_value=n1 / dt1)
 
 
 def main():
@@ -175,9 +242,19 @@ def main():
             el, km, er, _ = run_workload(E, rank, 1, args, sp, lm, mm, args.steps, args.warmup)
             secondary[name] = dict(env_steps_per_sec=E * args.steps / el, ms_per_step=km, err_envs=er)
             log(name, secondary[name])
+        E4 = CONFIG4["envs"]
+        el, km, er, _ = run_workload(E4, rank, 1, args, "config4", 0, 0, args.steps, args.warmup,
+                                     CONFIG4)
+        B4 = algorithmic_bytes(len(CONFIG4["blue"]), len(CONFIG4["red"]))
+        secondary["config4_8v10ls_g200"] = dict(
+            env_steps_per_sec=E4 * args.steps / el, ms_per_step=km, err_envs=er, envs=E4,
+            algorithmic_bytes_per_env_step=B4, achieved_GBs=B4 * E4 / (km * 1e-3) / 1e9)
+        log("config4", secondary["config4_8v10ls_g200"])
+        secondary["ray_march"] = ray_march()
+        log("ray_march", secondary["ray_march"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         line = {
             "metric": "env-steps/sec (whole node), 65536 parallel 4v4 envs on 100x100 grid",

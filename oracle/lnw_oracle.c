@@ -1093,8 +1093,20 @@ void orc_philox(uint64_t seed, uint64_t ctr, uint64_t gid, uint32_t *out) {
 /* stepped one after another for n_steps each with U[0,1) float32 actions,   */
 /* auto-reset when done == 0 or after `horizon` steps. Returns steps run.    */
 /* ------------------------------------------------------------------------ */
+int64_t orc_bench_range(const orc_params *P, const uint8_t *grid, int G, int nb, int nr,
+                        const int *types, const int *pos, int env0, int n_envs, int n_steps,
+                        int horizon, uint64_t seed);
+
 int64_t orc_bench(const orc_params *P, const uint8_t *grid, int G, int nb, int nr, const int *types,
                   const int *pos, int n_envs, int n_steps, int horizon, uint64_t seed) {
+    return orc_bench_range(P, grid, G, nb, nr, types, pos, 0, n_envs, n_steps, horizon, seed);
+}
+
+/* CPU-baseline driver over global env ids [env0, env0 + n_envs): no shared
+ * mutable state, so disjoint ranges can run on concurrent threads. */
+int64_t orc_bench_range(const orc_params *P, const uint8_t *grid, int G, int nb, int nr,
+                        const int *types, const int *pos, int env0, int n_envs, int n_steps,
+                        int horizon, uint64_t seed) {
     int A = nb + nr;
     orc_env *e = (orc_env *)malloc(sizeof(orc_env));
     double *act = (double *)malloc(sizeof(double) * 4 * A);
@@ -1104,7 +1116,7 @@ int64_t orc_bench(const orc_params *P, const uint8_t *grid, int G, int nb, int n
     double rb[ORC_MAX_AGENTS], rr[ORC_MAX_AGENTS], cog;
     int64_t steps = 0;
     for (int a = 0; a < A; a++) kinds[a] = K_F32;
-    for (int env = 0; env < n_envs; env++) {
+    for (int env = env0; env < env0 + n_envs; env++) {
         orc_env_init(e, P, grid, G, nb, nr);
         orc_set_rng(e, 0, seed, (uint64_t)env, 0, NULL, 0, 0);
         orc_reset(e, types, pos, NULL);
