@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs", type=int, default=65536, help="environments per GPU")
     p.add_argument("--spawns", choices=["reference", "melee"], default="reference")
+    p.add_argument("--workload", choices=["config3", "config4"], default="config3",
+                   help="config3 = the headline 4v4 line; config4 = 8v10+LS on 200x200 "
+                        "(diagnostics, e.g. with LNW_PROF=1)")
     p.add_argument("--los-mode", type=int, default=0, help="0 LOS table, 1 ray march")
     p.add_argument("--move-mode", type=int, default=0, help="0 move table, 1 direct A*")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -219,8 +222,11 @@ def main():
     torch.cuda.set_device(local)
     dist.init("nccl")
     E = args.envs
+    cfg = CONFIG4 if args.workload == "config4" else None
+    if cfg is not None and E == 65536:
+        E = cfg["envs"]
     elapsed, kms_mean, err, episodes = run_workload(
-        E, rank, world, args, args.spawns, args.los_mode, args.move_mode, args.steps, args.warmup)
+        E, rank, world, args, args.spawns, args.los_mode, args.move_mode, args.steps, args.warmup, cfg)
     elapsed, kms_mean = dist.reduce_max([elapsed, kms_mean])
     value = world * E * args.steps / elapsed
     nb = nr = 4

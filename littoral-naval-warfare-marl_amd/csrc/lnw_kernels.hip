@@ -236,6 +236,10 @@ struct ObsAcc {
   int obs_n, norder;
 };
 
+__device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int xj, int yj,
+                                      bool rad_ok, bool close, bool ew_cand, uint32_t los,
+                                      ObsAcc &acc);
+
 // One own-ship x opponent check of get_obs (combatant.py:106-124) once the
 // squared distance is known: radar / close / EW conditions, LOS (table or
 // march), the position-deduplicated observed list and EW bearings (gauss).
@@ -250,7 +254,17 @@ __device__ inline void pair_detect(Ctx &X, int myradar, int i, int jj, int xi, i
   bool close = d2 < 16;
   bool ew_cand = d2 < re * re && radj == 1;
   if (!(rad_ok || close || ew_cand)) return;  // LOS result would be unused
-  uint32_t los = los_q(P, S, X.mask, xi, yi, xj, yj);
+  pair_after_los(X, i, jj, xi, yi, xj, yj, rad_ok, close, ew_cand,
+                 los_q(P, S, X.mask, xi, yi, xj, yj), acc);
+}
+
+// The LOS-dependent part of one get_obs pair (combatant.py:106-124).
+__device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int xj, int yj,
+                                      bool rad_ok, bool close, bool ew_cand, uint32_t los,
+                                      ObsAcc &acc) {
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
   if (!(los & 1u)) return;
   uint32_t pk = pack_pos(xj, yj);
   bool seen = false;
@@ -279,6 +293,129 @@ __device__ inline void pair_detect(Ctx &X, int myradar, int i, int jj, int xi, i
 
 // Target list (combatant.py:152-161): observed positions first, then every EW
 // fix (combatant.py:128-150) landing within 2 cells of a live opponent.
+// Mean of the consecutive-pair EW fixes of opponent jj's n bearings
+// (combatant.py:128-150, calculate_fixed_position :265-277), summed in
+// np.mean's order (pairwise for >= 8 terms). Returns false on a zero slope
+// difference (the reference's ZeroDivisionError).
+struct FixAcc {
+  double sumx = 0, sumy = 0, resx = 0, resy = 0;
+  double r0x = 0, r1x = 0, r2x = 0, r3x = 0, r4x = 0, r5x = 0, r6x = 0, r7x = 0;
+  double r0y = 0, r1y = 0, r2y = 0, r3y = 0, r4y = 0, r5y = 0, r6y = 0, r7y = 0;
+  bool tail_started = false;
+  // every partial sum conditionally updated (no indexed array or address select,
+  // which would keep the sums in scratch); folds to one update for constant r
+  __device__ void put(int r, bool acc, double x3, double y3) {
+#define LNW_PUT(i)                                              \
+  r##i##x = r == i ? (acc ? r##i##x + x3 : x3) : r##i##x;      \
+  r##i##y = r == i ? (acc ? r##i##y + y3 : y3) : r##i##y;
+    LNW_PUT(0) LNW_PUT(1) LNW_PUT(2) LNW_PUT(3) LNW_PUT(4) LNW_PUT(5) LNW_PUT(6) LNW_PUT(7)
+#undef LNW_PUT
+  }
+  __device__ void add(int k, int m, double x3, double y3) {
+    const int mblk = m - (m % 8);
+    if (m < 8) {
+      sumx += x3;
+      sumy += y3;
+    } else if (k < mblk) {
+      put(k & 7, k >= 8, x3, y3);
+    } else {
+      if (!tail_started) { tree(); tail_started = true; }
+      resx += x3;
+      resy += y3;
+    }
+  }
+  __device__ void tree() {
+    resx = ((r0x + r1x) + (r2x + r3x)) + ((r4x + r5x) + (r6x + r7x));
+    resy = ((r0y + r1y) + (r2y + r3y)) + ((r4y + r5y) + (r6y + r7y));
+  }
+  __device__ void mean(int m, double &mx, double &my) {
+    if (m < 8) { mx = sumx / (double)m; my = sumy / (double)m; return; }
+    if (!tail_started) tree();
+    mx = resx / (double)m;
+    my = resy / (double)m;
+  }
+};
+
+__device__ inline void fix_pair(double m1, double m2, double x1, double y1, double x2, double y2,
+                                double &x3, double &y3) {
+  x3 = (m1 * x1 - m2 * x2 + y2 - y1) / (m1 - m2);
+  y3 = m1 * (x3 - x1) + y1;
+}
+
+// any n: one bearing pair at a time from the global scratch
+__device__ inline bool fix_mean_loop(Ctx &X, int jj, int n, double &mx, double &my) {
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  auto slot = [&](int k) { return (size_t)(jj * S.nmax + k) * X.E + X.env; };
+  const int m = n - 1;
+  FixAcc f;
+  for (int k = 0; k < m; k++) {
+    uint8_t s1 = S.bear_ship[slot(k)], s2 = S.bear_ship[slot(k + 1)];
+    double b1 = S.bear_val[slot(k)], b2 = S.bear_val[slot(k + 1)];
+    uint32_t p1 = COLW(c.pos_cur, s1), p2 = COLW(c.pos_cur, s2);
+    double m1 = tan(b1 * DEG2RAD);
+    double m2 = tan(b2 * DEG2RAD);
+    if (m1 - m2 == 0.0) return false;
+    double x3, y3;
+    fix_pair(m1, m2, pos_x(p1), pos_y(p1), pos_x(p2), pos_y(p2), x3, y3);
+    f.add(k, m, x3, y3);
+  }
+  f.mean(m, mx, my);
+  return true;
+}
+
+// n <= BMAX: all bearings loaded together, one tan per bearing, the pairs
+// unrolled (same arithmetic and summation order as fix_mean_loop)
+template <int BMAX>
+__device__ inline bool fix_mean_batched(Ctx &X, int jj, int n, double &mx, double &my) {
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  auto slot = [&](int k) { return (size_t)(jj * S.nmax + k) * X.E + X.env; };
+  double bv[BMAX];
+  int bs[BMAX];
+#pragma unroll
+  for (int k = 0; k < BMAX; k++) {
+    bv[k] = 0.0;
+    bs[k] = 0;
+    if (k < n) { bv[k] = S.bear_val[slot(k)]; bs[k] = S.bear_ship[slot(k)]; }
+  }
+  double tv[BMAX], px[BMAX], py[BMAX];
+#pragma unroll
+  for (int k = 0; k < BMAX; k++) {
+    tv[k] = 0.0;
+    px[k] = py[k] = 0.0;
+    if (k < n) {
+      tv[k] = tan(bv[k] * DEG2RAD);
+      const uint32_t p = COLW(c.pos_cur, bs[k]);
+      px[k] = pos_x(p);
+      py[k] = pos_y(p);
+    }
+  }
+  const int m = n - 1;
+  FixAcc f;
+  bool zero = false;
+#pragma unroll
+  for (int k = 0; k < BMAX - 1; k++) {
+    if (k < m && !zero) {
+      if (tv[k] - tv[k + 1] == 0.0) {
+        zero = true;
+      } else {
+        double x3, y3;
+        fix_pair(tv[k], tv[k + 1], px[k], py[k], px[k + 1], py[k + 1], x3, y3);
+        f.add(k, m, x3, y3);
+      }
+    }
+  }
+  if (zero) return false;
+  f.mean(m, mx, my);
+  return true;
+}
+
+// BMAX: bearings per opponent handled by the batched fix path; EXACT: no more
+// can occur (compile-time own-team size), so the loop fallback is not built.
+template <int BMAX, bool EXACT>
 __device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsAcc &acc) {
   const KParams &P = X.P;
   const KState &S = X.S;
@@ -300,75 +437,11 @@ __device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsA
     int jj = COLB(c.border, o);
     int n = COLB(c.bcnt, jj);
     if (n < 2) continue;
-    bool zero = false;
-    auto slot = [&](int k) { return (size_t)(jj * S.nmax + k) * E + env; };
-    // consecutive-pair fixes summed in np.mean's order (pairwise for >= 8)
-    double sumx = 0.0, sumy = 0.0;
-    int m = n - 1;
-    double r0x = 0, r1x = 0, r2x = 0, r3x = 0, r4x = 0, r5x = 0, r6x = 0, r7x = 0;
-    double r0y = 0, r1y = 0, r2y = 0, r3y = 0, r4y = 0, r5y = 0, r6y = 0, r7y = 0;
-    int mblk = m - (m % 8);
-    bool tail_started = false;
-    double resx = 0.0, resy = 0.0;
-    for (int k = 0; k < m; k++) {
-      uint8_t s1 = S.bear_ship[slot(k)], s2 = S.bear_ship[slot(k + 1)];
-      double b1 = S.bear_val[slot(k)], b2 = S.bear_val[slot(k + 1)];
-      uint32_t p1 = COLW(c.pos_cur, s1), p2 = COLW(c.pos_cur, s2);
-      double x1 = pos_x(p1), y1 = pos_y(p1), x2 = pos_x(p2), y2 = pos_y(p2);
-      // calculate_fixed_position (combatant.py:265-277)
-      double m1 = tan(b1 * DEG2RAD);
-      double m2 = tan(b2 * DEG2RAD);
-      if (m1 - m2 == 0.0) { zero = true; break; }
-      double x3 = (m1 * x1 - m2 * x2 + y2 - y1) / (m1 - m2);
-      double y3 = m1 * (x3 - x1) + y1;
-      if (m < 8) {
-        sumx += x3;
-        sumy += y3;
-      } else if (k < 8) {
-        switch (k) {
-          case 0: r0x = x3; r0y = y3; break;
-          case 1: r1x = x3; r1y = y3; break;
-          case 2: r2x = x3; r2y = y3; break;
-          case 3: r3x = x3; r3y = y3; break;
-          case 4: r4x = x3; r4y = y3; break;
-          case 5: r5x = x3; r5y = y3; break;
-          case 6: r6x = x3; r6y = y3; break;
-          default: r7x = x3; r7y = y3; break;
-        }
-      } else if (k < mblk) {
-        switch (k & 7) {
-          case 0: r0x += x3; r0y += y3; break;
-          case 1: r1x += x3; r1y += y3; break;
-          case 2: r2x += x3; r2y += y3; break;
-          case 3: r3x += x3; r3y += y3; break;
-          case 4: r4x += x3; r4y += y3; break;
-          case 5: r5x += x3; r5y += y3; break;
-          case 6: r6x += x3; r6y += y3; break;
-          default: r7x += x3; r7y += y3; break;
-        }
-      } else {
-        if (!tail_started) {
-          resx = ((r0x + r1x) + (r2x + r3x)) + ((r4x + r5x) + (r6x + r7x));
-          resy = ((r0y + r1y) + (r2y + r3y)) + ((r4y + r5y) + (r6y + r7y));
-          tail_started = true;
-        }
-        resx += x3;
-        resy += y3;
-      }
-    }
-    if (zero) { X.rng.err |= LNW_ERRF_ZERODIV; continue; }
     double mx, my;
-    if (m < 8) {
-      mx = sumx / (double)m;
-      my = sumy / (double)m;
-    } else {
-      if (!tail_started) {
-        resx = ((r0x + r1x) + (r2x + r3x)) + ((r4x + r5x) + (r6x + r7x));
-        resy = ((r0y + r1y) + (r2y + r3y)) + ((r4y + r5y) + (r6y + r7y));
-      }
-      mx = resx / (double)m;
-      my = resy / (double)m;
-    }
+    bool ok;
+    if constexpr (EXACT) ok = fix_mean_batched<BMAX>(X, jj, n, mx, my);
+    else ok = n <= BMAX ? fix_mean_batched<BMAX>(X, jj, n, mx, my) : fix_mean_loop(X, jj, n, mx, my);
+    if (!ok) { X.rng.err |= LNW_ERRF_ZERODIV; continue; }
     if (!isfinite(mx) || !isfinite(my)) { X.rng.err |= LNW_ERRF_NAN_ROUND; continue; }
     double rx = rint(mx), ry = rint(my);
     if (!(rx >= 0.0 && rx < (double)P.G && ry >= 0.0 && ry < (double)P.G)) continue;
@@ -392,32 +465,71 @@ __device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsA
 // written in phase O).
 __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   const KParams &P = X.P;
+  const KState &S = X.S;
   Cols &c = X.c;
   const int lane = X.lane;
   const int nb = P.nb, A = P.A;
   const int side = me >= nb;
   const int own0 = side ? nb : 0, own1 = side ? A : nb;
   const int opp0 = side ? 0 : nb, opp1 = side ? nb : A;
+  const int nopp = opp1 - opp0, npair = (own1 - own0) * nopp;
   const int myradar = COLW(c.radar_cur, me);
   ObsAcc acc{0, 0};
-  for (int q = 0; q < opp1 - opp0; q++) COLB(c.bcnt, q) = 0;
-  for (int i = own0; i < own1; i++) {
-    if (!COLB(c.alive0, i)) continue;
-    uint32_t pi = COLW(c.pos_cur, i);
-    int xi = pos_x(pi), yi = pos_y(pi);
-    int ti = COLB(c.type, i);
-    for (int j = opp0; j < opp1; j++) {
-      if (!COLB(c.alive0, j)) continue;
-      uint32_t pj = COLW(c.pos_cur, j);
-      int xj = pos_x(pj), yj = pos_y(pj);
-      int dx = xj - xi, dy = yj - yi;
-      int d2 = dx * dx + dy * dy;
+  for (int q = 0; q < nopp; q++) COLB(c.bcnt, q) = 0;
+  // pairs (i outer, j inner) in chunks of 16: the sensor tests of a chunk, then
+  // its LOS table words loaded together, then the chunk walked in order
+#pragma unroll 1
+  for (int b0 = 0; b0 < npair; b0 += 16) {
+    uint32_t radm = 0, closem = 0, ewm = 0, tabm = 0, marchm = 0;
+    uint32_t wi[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      wi[u] = 0;
+      const int b = b0 + u;
+      if (b >= npair) continue;
+      const int i = own0 + b / nopp, j = opp0 + b % nopp;
+      if (!COLB(c.alive0, i) || !COLB(c.alive0, j)) continue;
+      const uint32_t pi = COLW(c.pos_cur, i), pj = COLW(c.pos_cur, j);
+      const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
+      const int d2 = dx * dx + dy * dy;
       if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
-      pair_detect(X, myradar, i, j - opp0, xi, yi, ti, xj, yj, COLB(c.type, j),
-                  COLW(c.radar_cur, j), d2, acc);
+      const int ti = COLB(c.type, i), tj = COLB(c.type, j);
+      const int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
+      const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
+      const bool ew_cand = d2 < re * re && COLW(c.radar_cur, j) == 1;
+      if (!(rad_ok || close || ew_cand)) continue;  // LOS result would be unused
+      radm |= (rad_ok ? 1u : 0u) << u;
+      closem |= (close ? 1u : 0u) << u;
+      ewm |= (ew_cand ? 1u : 0u) << u;
+      if (P.los_mode == 0 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS) {
+        tabm |= 1u << u;
+        wi[u] = ((uint32_t)(pos_x(pi) * P.G + pos_y(pi)) * LOS_CELL_WORDS + (dx + R_LOS) * LOS_ROW_WORDS) *
+                    32u + (dy + R_LOS) * 2;
+      } else {
+        marchm |= 1u << u;
+      }
+    }
+    uint32_t losb = 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const uint32_t w = (tabm >> u) & 1u ? S.lostab[wi[u] >> 5] : 0u;
+      losb |= ((w >> (wi[u] & 31)) & 3u) << (2 * u);
+    }
+    uint32_t todo = tabm | marchm;
+    while (todo) {
+      const int u = __builtin_ctz(todo);
+      todo &= todo - 1;
+      const int b = b0 + u;
+      const int i = own0 + b / nopp, j = opp0 + b % nopp;
+      const uint32_t pi = COLW(c.pos_cur, i), pj = COLW(c.pos_cur, j);
+      const int xi = pos_x(pi), yi = pos_y(pi), xj = pos_x(pj), yj = pos_y(pj);
+      const uint32_t los = (tabm >> u) & 1u ? (losb >> (2 * u)) & 3u
+                                            : los_q(P, S, X.mask, xi, yi, xj, yj);
+      pair_after_los(X, i, j - opp0, xi, yi, xj, yj, (radm >> u) & 1u, (closem >> u) & 1u,
+                     (ewm >> u) & 1u, los, acc);
     }
   }
-  finish_obs(X, me, opp0, opp1, acc);
+  finish_obs<16, false>(X, me, opp0, opp1, acc);
 }
 
 // Compile-time ship counts: positions and alive flags of both sides are read
@@ -464,7 +576,7 @@ __device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
     pair_detect(X, myradar, own0 + i, j, xi, yi, COLB(c.type, own0 + i), xj, yj,
                 COLB(c.type, opp0 + j), COLW(c.radar_cur, opp0 + j), dx * dx + dy * dy, acc);
   }
-  finish_obs(X, me, opp0, opp0 + NOPP, acc);
+  finish_obs<NOWN, true>(X, me, opp0, opp0 + NOPP, acc);
 }
 
 // check_target (combatant.py:570-584): first live opponent within 3.5 cells
