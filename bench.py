@@ -169,6 +169,37 @@ def ray_march(n=1 << 22, reps=10):
                 rays=n, mean_cells_per_ray=cells / n)
 
 
+def mappo_rollout(E=32768, T=40, reps=3):
+    """SURVEY.md §8(d) config 5 on one GPU: 40-step MAPPO rollouts of E envs, the
+    batched actor (network.py MLP) acting for every blue ship and the critic
+    scoring every step, interleaved with the step kernel (lnw.rollout.Rollout,
+    scripted red). env-steps/s including the policy forwards."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    from lnw.rollout import BatchedActor, BatchedCritic, Rollout
+    sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=False,
+                  auto_reset=True, episode_steps=40)
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc,
+                    device=torch.cuda.current_device(), seed=77)
+    torch.manual_seed(0)
+    actor = BatchedActor.for_obs(g.Db).cuda()
+    critic = BatchedCritic(g.Db * g.nb).cuda()
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    r = Rollout(g, actor, critic, steps=T, noise=0.05)
+    g.reset(positions=REF_BLUE + REF_RED)
+    r.run(generator=gen)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.reset(positions=REF_BLUE + REF_RED)
+        r.run(generator=gen)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    g.close()
+    return dict(env_steps_per_sec=E * T / dt, ms_per_rollout=dt * 1e3, envs=E, steps=T,
+                policy="batched actor (network.py MLP) + critic (Value), fp32")
+
+
 def cpu_baseline(seconds, threads):
     """The CPU oracle (oracle/lnw_oracle.c, a C restatement of the reference
     step) timed on the host over a bounded sample of the same workload: one
@@ -258,6 +289,8 @@ def main():
         log("config4", secondary["config4_8v10ls_g200"])
         secondary["ray_march"] = ray_march()
         log("ray_march", secondary["ray_march"])
+        secondary["config5_mappo_rollout"] = mappo_rollout()
+        log("config5", secondary["config5_mappo_rollout"])
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)

@@ -1,0 +1,262 @@
+"""On-device MAPPO rollout pieces around the batched step (SURVEY.md §8(f) rows
+1-3): the reference's actor / critic evaluated for every (env, ship) at once,
+rollout storage as [E, T, ...] device tensors, the reference's reward-to-go and
+GAE as batched tensor ops, and the scripted red action profiles as a device
+table. Observations never leave the GPU.
+
+Reference: ppo.py:421-671 (rollout), network.py:38-172 (MLP, Value),
+ppo.py:645-659 (reward-to-go), ppo.py:695-714 (gae), game.py:173-182 and
+536-542 (red_steps*.csv profiles).
+"""
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.distributions import Normal
+
+from .batched import BatchedGame
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+WINDOW = 49  # the 7x7 terrain window at the head of a Combatant observation
+
+
+class BatchedActor(nn.Module):
+    """network.py:38-152 `MLP` for a [B, D] batch of observations.
+
+    Same submodules, parameter names and initialisation as the reference, so a
+    reference `state_dict` loads as is (`load_reference`). The reference is a
+    batch-1 network: it flattens the conv head over the batch and concatenates
+    along dim 0 (network.py:83), and the PPO rollout calls it one state at a time
+    with BatchNorm in training mode (ppo.py:504-512), i.e. with statistics of that
+    single sample. `bn="sample"` reproduces exactly that for every row (instance
+    statistics with the BatchNorm affine parameters); `bn="running"` is the
+    eval-mode network (running statistics). Running statistics are not updated.
+    """
+
+    def __init__(self, n_inputs, n_outputs):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 5, 3, 1, padding=1)
+        self.norm1 = nn.BatchNorm2d(5)
+        self.pool = nn.MaxPool2d(2, 2)
+        self.conv2 = nn.Conv2d(5, 8, 3, 1, padding=1)
+        self.norm2 = nn.BatchNorm2d(8)
+        self.pool2 = nn.MaxPool2d(2, 2)
+        self.convhead = nn.Linear(8, 12, bias=True)
+        self.layernorm = nn.LayerNorm(n_inputs)
+        self.fc1 = nn.Linear(n_inputs, 64, bias=True)
+        self.fc2 = nn.Linear(64, 64, bias=True)
+        self.fc3 = nn.Linear(64, 32, bias=True)
+        self.normal_head = nn.Linear(32, n_outputs, bias=False)
+        self.log_std_head = nn.Linear(32, n_outputs, bias=False)
+        for m in (self.fc1, self.fc2, self.fc3, self.normal_head, self.log_std_head):
+            nn.init.xavier_uniform_(m.weight)
+        self.logstd = nn.Parameter(torch.zeros(()))  # present in the reference, unused there too
+
+    @classmethod
+    def for_obs(cls, obs_dim, n_outputs=4):
+        """The reference sizing: n_inputs = obs_dim - 7*7 + 12 (ppo.py:78, 446)."""
+        return cls(obs_dim - WINDOW + 12, n_outputs)
+
+    def load_reference(self, state_dict):
+        """Load a reference MLP state_dict (tensors or arrays)."""
+        sd = {k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()}
+        if "logstd" not in sd:
+            sd["logstd"] = torch.zeros(())
+        self.load_state_dict({k: v.reshape(self.state_dict()[k].shape) for k, v in sd.items()})
+        return self
+
+    @staticmethod
+    def _bn(m, z, bn):
+        if bn == "sample":
+            return F.instance_norm(z, weight=m.weight, bias=m.bias, eps=m.eps)
+        return F.batch_norm(z, m.running_mean, m.running_var, m.weight, m.bias, False, 0.0, m.eps)
+
+    def heads(self, obs, bn="sample"):
+        """(normal mean, normal std) for every row of obs [B, D]."""
+        B = obs.shape[0]
+        z = obs[:, :WINDOW].reshape(B, 1, 7, 7)
+        z = self.pool(F.relu(self._bn(self.norm1, self.conv1(z), bn)))
+        z = self.pool2(F.relu(self._bn(self.norm2, self.conv2(z), bn)))
+        z = self.convhead(torch.flatten(z, 1))
+        x = self.layernorm(torch.cat((z, obs[:, WINDOW:]), 1))
+        x = torch.tanh(self.fc1(x))
+        x = torch.tanh(self.fc2(x))
+        x = torch.tanh(self.fc3(x))
+        return torch.tanh(self.normal_head(x)), torch.exp(self.log_std_head(x))
+
+    def forward(self, obs, noise=None, bn="sample", generator=None):
+        """network.py:70-115 for every row: sample N(mean, std), add N(0, noise)
+        exploration noise, clamp to [0, 1], log-probabilities of the clamped
+        actions. Returns (actions, log_probs, ok) where ok marks rows without
+        NaN heads (the reference returns (None, None) for those)."""
+        mean, std = self.heads(obs, bn)
+        ok = ~(torch.isnan(mean).any(1) | torch.isnan(std).any(1))
+        mean_s = torch.where(ok[:, None], mean, torch.zeros_like(mean))
+        std_s = torch.where(ok[:, None], std, torch.ones_like(std))
+        dist = Normal(mean_s, std_s)
+        eps = torch.randn(mean.shape, generator=generator, device=mean.device, dtype=mean.dtype)
+        actions = mean_s + std_s * eps
+        if noise is not None:
+            actions = actions + noise * torch.randn(mean.shape, generator=generator,
+                                                    device=mean.device, dtype=mean.dtype)
+        actions = torch.clamp(actions, 0, 1)
+        return actions, dist.log_prob(actions), ok
+
+    def get_dist(self, obs, actions, bn="sample"):
+        """network.py:117-152: (log_probs, entropies) of given actions."""
+        mean, std = self.heads(obs, bn)
+        dist = Normal(mean, std)
+        return dist.log_prob(actions), dist.entropy()
+
+
+class BatchedCritic(nn.Module):
+    """network.py:154-172 `Value` (already batched in the reference): the
+    centralised critic over the concatenated observations of one side."""
+
+    def __init__(self, n_inputs):
+        super().__init__()
+        self.fc1 = nn.Linear(n_inputs, 32, bias=True)
+        self.fc2 = nn.Linear(32, 64, bias=True)
+        self.fc3 = nn.Linear(64, 64, bias=True)
+        self.fc4 = nn.Linear(64, 1)
+        for m in (self.fc1, self.fc2, self.fc3, self.fc4):
+            nn.init.xavier_uniform_(m.weight)
+
+    def load_reference(self, state_dict):
+        self.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()})
+        return self
+
+    def forward(self, x):
+        x = torch.flatten(x, 1)
+        x = torch.tanh(self.fc1(x))
+        x = torch.tanh(self.fc2(x))
+        x = torch.tanh(self.fc3(x))
+        return self.fc4(x)
+
+
+def red_script_table(device="cuda", dtype=torch.float32):
+    """The scripted red profiles (red_steps.csv, red_steps2.csv, red_steps3.csv;
+    game.py:173-182) as a device tensor [3, 40, 4] = [red ship, step, action]."""
+    return torch.as_tensor(np.load(os.path.join(DATA, "red_steps.npy")), dtype=dtype, device=device)
+
+
+def red_script_actions(table, step, n_red):
+    """Red actions of one step for untrained red (ppo.py:560-565): profile i for
+    red ship i < 3; ships beyond the three profiles, and steps past the 40 rows,
+    get zero actions (the reference indexes past its lists there)."""
+    out = torch.zeros((n_red, 4), dtype=table.dtype, device=table.device)
+    if step < table.shape[1]:
+        k = min(n_red, table.shape[0])
+        out[:k] = table[:k, step]
+    return out
+
+
+def reference_rtg(rewards, gamma):
+    """ppo.py:645-659 reward-to-go for rollouts rewards [R, T, n] (one rollout
+    per leading index), as the reference computes it. The loop walks the steps
+    in reverse and the ships in order, `discounted_reward += gamma * r`, and
+    appends the accumulator after every term; the reward buffer has a trailing
+    dim of 1, so after the first term the accumulator is a 1-element ndarray
+    updated in place and every appended entry is that same array. Every element
+    of the result is therefore gamma * (sum of the rollout's rewards), summed in
+    that order. Returned as float64 [R, T, n], like the reference's buffer."""
+    R, T, n = rewards.shape
+    rev = torch.flip(rewards.to(torch.float64), dims=[1]).reshape(R, T * n)
+    total = torch.cumsum(gamma * rev, dim=1)[:, -1]
+    return total[:, None, None].expand(R, T, n).contiguous()
+
+
+def discounted_rtg(rewards, gamma):
+    """Per-ship discounted return G_t = r_t + gamma * G_{t+1} over [R, T, n]
+    (what the reference's loop is meant to compute; not used by it)."""
+    out = torch.zeros_like(rewards, dtype=torch.float64)
+    acc = torch.zeros_like(rewards[:, 0], dtype=torch.float64)
+    for t in reversed(range(rewards.shape[1])):
+        acc = rewards[:, t].to(torch.float64) + gamma * acc
+        out[:, t] = acc
+    return out
+
+
+def gae(rewards, values, gamma, lambda_=0.95):
+    """ppo.py:695-714 generalised advantage estimate, batched over leading dims
+    (the sequence runs along the last dim), same operation order."""
+    returns = torch.zeros_like(rewards)
+    n = rewards.shape[-1]
+    g = torch.zeros_like(rewards[..., 0])
+    for i in reversed(range(n)):
+        if i < n - 1:
+            delta = rewards[..., i] + gamma * values[..., i + 1] - values[..., i]
+            g = delta + gamma * lambda_ * g
+        else:
+            delta = rewards[..., i] - values[..., i]
+            g = delta
+        returns[..., i] = g + values[..., i]
+    return returns
+
+
+class Rollout:
+    """Batched MAPPO rollout (ppo.py:421-671 with the side being trained = blue):
+    every step, the actor acts for all blue ships of all envs from the previous
+    step's observations, red acts from the scripted profiles (untrained red) or
+    a red actor, the step kernel advances all envs, and the critic scores the
+    concatenated blue observations. Buffers are device tensors [E, T, ...].
+
+    Differences from the reference loop, by design: observations come from the
+    step outputs (plus one `observe` at the start) instead of fresh
+    `ship.get_obs()` calls on the main env (ppo.py:497-500 observes the wrong
+    env); with `stop_at_done` rewards after an env's first `done == 0` are
+    zeroed, as the reference's zero-initialised buffers are after its `break`.
+    """
+
+    def __init__(self, game: BatchedGame, actor, critic=None, steps=40, red="script",
+                 red_actor=None, noise=None, bn="sample", gamma=0.99, stop_at_done=True):
+        self.g, self.actor, self.critic = game, actor, critic
+        self.T, self.red, self.red_actor = int(steps), red, red_actor
+        self.noise, self.bn, self.gamma, self.stop_at_done = noise, bn, float(gamma), stop_at_done
+        self.table = red_script_table(game.device) if red == "script" else None
+
+    @torch.no_grad()
+    def run(self, generator=None):
+        g = self.g
+        E, nb, nr, A, D = g.E, g.nb, g.nr, g.A, g.Db
+        dev = g.device
+        T = self.T
+        obs = torch.empty((E, T, nb, D), dtype=torch.float32, device=dev)
+        acts = torch.empty((E, T, nb, 4), dtype=torch.float32, device=dev)
+        logp = torch.empty((E, T, nb, 4), dtype=torch.float32, device=dev)
+        rew = torch.zeros((E, T, nb), dtype=torch.float32, device=dev)
+        val = torch.zeros((E, T), dtype=torch.float32, device=dev)
+        running = torch.ones((E, T), dtype=torch.bool, device=dev)
+        full = torch.zeros((E, A, 4), dtype=torch.float32, device=dev)
+        cur = g.observe(-1)[0].clone()
+        live = torch.ones(E, dtype=torch.bool, device=dev)
+        for t in range(T):
+            obs[:, t] = cur
+            a, lp, _ = self.actor(cur.reshape(E * nb, D), noise=self.noise, bn=self.bn,
+                                  generator=generator)
+            acts[:, t] = a.reshape(E, nb, 4)
+            logp[:, t] = lp.reshape(E, nb, 4)
+            full[:, :nb] = acts[:, t]
+            if self.red == "script":
+                full[:, nb:] = red_script_actions(self.table, t, nr)
+            elif self.red_actor is not None:
+                ra, _, _ = self.red_actor(g.obs_red.reshape(E * nr, g.Dr), bn=self.bn,
+                                          generator=generator)
+                full[:, nb:] = ra.reshape(E, nr, 4)
+            else:
+                full[:, nb:] = 0
+            if self.critic is not None:
+                val[:, t] = self.critic(cur.reshape(E, nb * D)).reshape(E)
+            out = g.step(full)
+            running[:, t] = live
+            r = out["rew_blue"]
+            rew[:, t] = torch.where(live[:, None], r, torch.zeros_like(r)) if self.stop_at_done else r
+            if self.stop_at_done:
+                live = live & (out["done"] != 0)
+            cur = out["obs_blue"].clone()
+        rtg = reference_rtg(rew, self.gamma)
+        return dict(obs=obs, actions=acts, log_probs=logp, rewards=rew, values=val,
+                    running=running, rtg=rtg,
+                    gae=gae(rew.mean(2), val, self.gamma) if self.critic is not None else None)

@@ -1,0 +1,91 @@
+"""Batched MAPPO rollout on the GPU (lnw.rollout.Rollout):
+buffers consistent with the step outputs, the device actor equal to the CPU
+actor, reference reward-to-go identity."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "littoral-naval-warfare-marl_amd"))
+
+pytestmark = pytest.mark.gpu
+
+REF_BLUE = [(6, 61), (10, 81), (8, 70), (11, 58)]
+REF_RED = [(98, 48), (98, 52), (98, 56), (96, 52)]
+
+
+def _game(E, seed=3):
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    sc = Scenario(landing_ops=False, auto_reset=False, trained_red=False)
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, seed=seed)
+    g.reset(positions=REF_BLUE + REF_RED, box=((40, 40), (57, 65)))
+    return g
+
+
+def test_actor_device_matches_cpu():
+    from lnw.rollout import BatchedActor
+    torch.manual_seed(0)
+    a = BatchedActor.for_obs(68)
+    obs = torch.rand(4096, 68)
+    with torch.no_grad():
+        m0, s0 = a.heads(obs)
+        m1, s1 = a.cuda().heads(obs.cuda())
+    np.testing.assert_allclose(m1.cpu().numpy(), m0.numpy(), atol=1e-5)
+    np.testing.assert_allclose(s1.cpu().numpy(), s0.numpy(), rtol=1e-5)
+
+
+def test_rollout_buffers():
+    from lnw.rollout import BatchedActor, BatchedCritic, Rollout, reference_rtg
+    E, T = 256, 12
+    g = _game(E)
+    torch.manual_seed(1)
+    actor = BatchedActor.for_obs(g.Db).cuda()
+    critic = BatchedCritic(g.Db * g.nb).cuda()
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    r = Rollout(g, actor, critic, steps=T, noise=0.05, gamma=0.99)
+    out = r.run(generator=gen)
+    assert out["obs"].shape == (E, T, 4, 68) and out["actions"].shape == (E, T, 4, 4)
+    a = out["actions"]
+    assert float(a.min()) >= 0 and float(a.max()) <= 1
+    for k in ("obs", "log_probs", "values"):
+        assert torch.isfinite(out[k]).all(), k
+    # the critic scored exactly the stored observations
+    with torch.no_grad():
+        v = critic(out["obs"].reshape(E * T, -1)).reshape(E, T)
+    torch.testing.assert_close(v, out["values"])
+    # the final step's outputs are the live buffers of the game
+    last = out["obs"][:, -1]
+    assert torch.isfinite(last).all()
+    rtg = out["rtg"]
+    want = reference_rtg(out["rewards"], 0.99)
+    torch.testing.assert_close(rtg, want)
+    assert torch.allclose(rtg[:, 0, 0], 0.99 * out["rewards"].double().sum((1, 2)))
+    g.close()
+
+
+def test_rollout_replays_with_stepped_actions():
+    """Stepping a second game with the rollout's recorded actions reproduces the
+    recorded observations (same seed, scripted red)."""
+    from lnw.rollout import BatchedActor, Rollout, red_script_actions, red_script_table
+    E, T = 128, 8
+    g1, g2 = _game(E, seed=9), _game(E, seed=9)
+    torch.manual_seed(2)
+    actor = BatchedActor.for_obs(68).cuda()
+    out = Rollout(g1, actor, None, steps=T, stop_at_done=False).run(
+        generator=torch.Generator(device="cuda").manual_seed(4))
+    g2.observe(-1)
+    tab = red_script_table()
+    full = torch.zeros((E, 8, 4), device="cuda")
+    for t in range(T):
+        full[:, :4] = out["actions"][:, t]
+        full[:, 4:] = red_script_actions(tab, t, 4)
+        o = g2.step(full)
+        if t + 1 < T:
+            torch.testing.assert_close(o["obs_blue"], out["obs"][:, t + 1], rtol=0, atol=0)
+        torch.testing.assert_close(o["rew_blue"], out["rewards"][:, t], rtol=0, atol=0)
+    g1.close()
+    g2.close()
