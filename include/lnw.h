@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define LNW_ABI_VERSION 1
+#define LNW_ABI_VERSION 2
 
 /* status codes */
 #define LNW_OK 0
@@ -209,6 +209,33 @@ int lnw_copy(void *dst, const void *src, int64_t nbytes, void *stream);
 /* Philox U[0,1) float32 fill keyed by (seed, offset + i): synthetic actions. */
 int lnw_fill_uniform_f32(float *out_dev, int64_t n, uint64_t seed, uint64_t offset,
                          void *stream);
+
+/* ---- analytics side channels ----------------------
+ * Device counterparts of Game.heatmap / coldmap / launch_sites / engagements /
+ * blue_ew / red_ew (game.py:119-154; written at combatant.py:640-657 and
+ * 146-150), accumulated over every env and step while bound. Each pointer may
+ * be NULL (that channel is off); lnw_set_analytics(h, NULL) turns all off.
+ * Maps are indexed [x * 100 + y] like the reference's 100x100 arrays (cells
+ * outside them are skipped). Log records are 4 x uint32:
+ *   engagement: env, step | side << 16 | missiles << 24, shooter x | y << 16,
+ *               target x | y << 16          (every hit; missiles 0 = main gun)
+ *   EW fix:     env, step | side << 16, observer x | y << 16,
+ *               (uint16)fix_x | (uint16)fix_y << 16   (every finite EW fix)
+ * with env the global env id, step the episode step (0-based) and side 0 blue /
+ * 1 red. *_count are incremented atomically per record; records past *_cap are
+ * counted but not stored. */
+typedef struct lnw_analytics {
+  uint32_t *heatmap;   /* [100*100] shooter cells of missile hits by the params.side side */
+  uint32_t *coldmap;   /* [100*100] target cells of those hits */
+  uint32_t *launch;    /* [2][100*100] missile-hit launch cells (blue, red) */
+  uint32_t *eng_log;   /* [eng_cap][4] */
+  uint32_t *eng_count; /* [1] */
+  int64_t eng_cap;
+  uint32_t *ew_log;    /* [ew_cap][4] */
+  uint32_t *ew_count;  /* [1] */
+  int64_t ew_cap;
+} lnw_analytics;
+int lnw_set_analytics(lnw_handle *h, const lnw_analytics *a);
 
 /* Host-side constants the kernels use (for tests): hit probability tables
  * 1-(1-p)^n for p in {0.45, 0.63}, n = 0..8, in float64 and float32. */

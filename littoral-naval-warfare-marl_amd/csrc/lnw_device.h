@@ -72,7 +72,8 @@ struct KState {
   const float *gridf;      // [G][G] grid/255 as float32
   const float *winf;       // [2][G*G][52] Combatant | LandingShip observation windows
   float *dummy;            // [WAVE * 4] sink for masked-out stores (keeps store counts static)
-  unsigned long long *prof;  // diagnostics (LNW_PROF): [n_wg][8] phase timestamps, else null
+  unsigned long long *prof;  // diagnostics (LNW_PROF): [n_wg][16] phase timestamps, else null
+  lnw_analytics ana;         // analytics side channels (null pointers: off)
   const uint32_t *mask2;   // [G][W16] 2 bits per cell: bit0 > move_thr, bit1 > ew_thr
   const uint32_t *mvtab;   // [2][G*G][3]
   const uint32_t *lostab;  // [G*G][486]

@@ -177,7 +177,22 @@ struct Ctx {
   const uint32_t *mask;  // LDS (march mode) or global
   long long E;
   int r2max;             // max over ship-type pairs of radar^2, EW^2 and 16 (d < 4)
+  int step;              // episode step being played (analytics records)
 };
+
+// analytics (lnw_set_analytics): one 4-word record appended to a capped log
+__device__ inline void ana_record(uint32_t *log, uint32_t *count, long long cap, uint32_t w0,
+                                  uint32_t w1, uint32_t w2, uint32_t w3) {
+  const uint32_t i = atomicAdd(count, 1u);
+  if ((long long)i < cap) {
+    uint4 *r = (uint4 *)log + i;
+    *r = make_uint4(w0, w1, w2, w3);
+  }
+}
+__device__ inline void ana_map(uint32_t *map, uint32_t p) {
+  const int x = pos_x(p), y = pos_y(p);
+  if (map && x < 100 && y < 100) atomicAdd(&map[x * 100 + y], 1u);
+}
 
 __device__ inline int max_range2(const KParams &P, double duct) {
   int m = 16;
@@ -444,6 +459,12 @@ __device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsA
     if (!ok) { X.rng.err |= LNW_ERRF_ZERODIV; continue; }
     if (!isfinite(mx) || !isfinite(my)) { X.rng.err |= LNW_ERRF_NAN_ROUND; continue; }
     double rx = rint(mx), ry = rint(my);
+    if (S.ana.ew_log) {  // combatant.py:146-150: (observer position, rounded fix)
+      const int fx = (int)fmin(fmax(rx, -32768.0), 32767.0), fy = (int)fmin(fmax(ry, -32768.0), 32767.0);
+      ana_record(S.ana.ew_log, S.ana.ew_count, S.ana.ew_cap, (uint32_t)(P.env_base + env),
+                 (uint32_t)X.step | (uint32_t)(me >= P.nb) << 16, COLW(c.pos_cur, me),
+                 (uint32_t)(uint16_t)fx | (uint32_t)(uint16_t)fy << 16);
+    }
     if (!(rx >= 0.0 && rx < (double)P.G && ry >= 0.0 && ry < (double)P.G)) continue;
     int fxi = (int)rx, fyi = (int)ry;
     for (int j = opp0; j < opp1; j++) {
@@ -609,7 +630,8 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
   if (t < 0) return false;
   uint32_t pt = COLW(c.pos_cur, t), pa = COLW(c.pos_cur, a);
   int dx = pos_x(pt) - pos_x(pa), dy = pos_y(pt) - pos_y(pa);
-  bool hit = false;
+  bool hit = false, missile = false;
+  int n = 0;  // missiles fired (0: main gun)
   if (dx * dx + dy * dy < 4) {
     hit = true;  // main gun, no draw
   } else {
@@ -635,7 +657,7 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
       kn = K_PYINT;
     }
     if (num > (double)miss) { num = (double)miss; kn = mk; }
-    int n = (int)num;
+    n = (int)num;
     COLB(c.miss_cur, a) = (uint8_t)(miss - n);
     COLB(c.mkind, a) = (uint8_t)kind_promote(mk, kn);
     double u2 = X.rng.uniform();
@@ -644,8 +666,20 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
       hit = (float)u2 < hit_sel(P.hit32, hp, n);
     else
       hit = u2 < hit_sel(P.hit64, hp, n);
+    missile = true;
   }
   if (hit) {
+    const KState &S = X.S;
+    if (missile) {  // combatant.py:642-652: maps of the trained side, launch sites of both
+      if (side == (P.side_blue ? 0 : 1)) {
+        ana_map(S.ana.heatmap, pa);
+        ana_map(S.ana.coldmap, pt);
+      }
+      if (S.ana.launch) ana_map(S.ana.launch + side * 10000, pa);
+    }
+    if (S.ana.eng_log)  // combatant.py:656-657
+      ana_record(S.ana.eng_log, S.ana.eng_count, S.ana.eng_cap, (uint32_t)(P.env_base + X.env),
+                 (uint32_t)X.step | (uint32_t)side << 16 | (uint32_t)n << 24, pa, pt);
     int ts = t >= P.nb;
     N.cnt[ts]++;
     N.mask[ts] |= 1u << (t - (ts ? P.nb : 0));
@@ -1467,11 +1501,12 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   if (valid && !(P.dbg_skip & 2)) {
     if (emit) publish_progress(&prog, 0);
     Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), emit ? S.mask2 : mask, E,
-          max_range2(P, duct)};
+          max_range2(P, duct), 0};
     Neut N{{0, 0}, {0u, 0u}};
     int ev[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) ev[q] = S.envi[q * E + env];
+    X.step = ev[2];
     int hits[2] = {0, 0};
     double bsx = 0, bsy = 0, rsx = 0, rsy = 0;
     int nbp = 0, nrp = 0;
@@ -1679,7 +1714,8 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   duct_col[lane] = duct;
   __syncthreads();
   if (valid) {
-    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E, max_range2(P, duct)};
+    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E, max_range2(P, duct),
+          S.envi[2 * E + env]};
     int a0 = 0, a1 = A;
     if (sel >= 0) { a0 = sel; a1 = sel + 1; }
     else if (sel == LNW_OBS_BLUE) { a1 = nb; }
@@ -1917,6 +1953,7 @@ struct lnw_handle {
   uint8_t *d_grid = nullptr;
   float *d_gridf = nullptr, *d_winf = nullptr, *d_dummy = nullptr;
   unsigned long long *d_prof = nullptr;  // LNW_PROF phase timestamps
+  lnw_analytics ana{};                   // bound analytics buffers (lnw_set_analytics)
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
   bool prof = false, force_generic = false;
@@ -1954,7 +1991,7 @@ KState make_state(lnw_handle *h) {
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
   s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
-  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.ana = h->ana; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
   s.sp_pos_env = nullptr;
@@ -2008,6 +2045,15 @@ extern "C" {
 
 int lnw_abi_version(void) { return LNW_ABI_VERSION; }
 const char *lnw_last_error(void) { return g_err.c_str(); }
+
+int lnw_set_analytics(lnw_handle *h, const lnw_analytics *a) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  if (!a) { h->ana = lnw_analytics{}; return 0; }
+  if ((a->eng_log && (!a->eng_count || a->eng_cap < 0)) || (a->ew_log && (!a->ew_count || a->ew_cap < 0)))
+    return fail(LNW_EINVAL, "analytics log without a counter or with a negative capacity");
+  h->ana = *a;
+  return 0;
+}
 
 int lnw_hit_tables(double *tab64, float *tab32) {
   KParams k{};

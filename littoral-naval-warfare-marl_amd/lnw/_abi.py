@@ -25,8 +25,14 @@ SYMBOLS = [
     "lnw_abi_version", "lnw_last_error", "lnw_create", "lnw_destroy", "lnw_load_terrain",
     "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_state_field", "lnw_tlist_cap",
     "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
-    "lnw_fill_uniform_f32", "lnw_hit_tables",
+    "lnw_fill_uniform_f32", "lnw_hit_tables", "lnw_set_analytics",
 ]
+
+
+class Analytics(C.Structure):  # include/lnw.h: lnw_analytics
+    _fields_ = [("heatmap", C.c_void_p), ("coldmap", C.c_void_p), ("launch", C.c_void_p),
+                ("eng_log", C.c_void_p), ("eng_count", C.c_void_p), ("eng_cap", C.c_int64),
+                ("ew_log", C.c_void_p), ("ew_count", C.c_void_p), ("ew_cap", C.c_int64)]
 
 
 class Params(C.Structure):
@@ -81,6 +87,7 @@ def load(path=None):
         "lnw_copy": ([P, P, I64, P], C.c_int),
         "lnw_fill_uniform_f32": ([P, I64, U64, U64, P], C.c_int),
         "lnw_hit_tables": ([P, P], C.c_int),
+        "lnw_set_analytics": ([P, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

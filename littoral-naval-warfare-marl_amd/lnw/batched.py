@@ -89,6 +89,7 @@ class BatchedGame:
         self.done = torch.ones((self.E,), dtype=torch.int32, device=dev)
         self.cog = torch.zeros((self.E,), dtype=torch.float32, device=dev)
         self._spawn = None
+        self._ana = None
         # step() hot path: output pointers and the accepted action layout, cached
         self._outp = tuple(_ptr(t) for t in (self.obs_blue, self.obs_red, self.rew_blue,
                                              self.rew_red, self.done, self.cog))
@@ -164,6 +165,64 @@ class BatchedGame:
         check(self.L.lnw_step(self.h, a.data_ptr(), dt, rk, ob, orr, rb, rr, dn, cg,
                               torch.cuda.current_stream(self.device).cuda_stream))
         return self._outd
+
+    # ---------------------------------------------------------- analytics
+    def enable_analytics(self, eng_cap=1 << 20, ew_cap=1 << 20, maps=True):
+        """Bind device buffers for the reference's analytics side channels
+        (heatmap / coldmap / launch sites / engagements / blue_ew / red_ew,
+        game.py:119-154) accumulated over all envs and steps (lnw_set_analytics).
+        maps=False binds the two logs only (the maps follow from the records)."""
+        dev = self.device
+        z = lambda *s: torch.zeros(s, dtype=torch.int32, device=dev)  # noqa: E731
+        self._ana = dict(heatmap=z(100, 100) if maps else None,
+                         coldmap=z(100, 100) if maps else None,
+                         launch=z(2, 100, 100) if maps else None,
+                         eng_log=z(max(1, eng_cap), 4), eng_count=z(1),
+                         ew_log=z(max(1, ew_cap), 4), ew_count=z(1))
+        t = self._ana
+        p = lambda k: t[k].data_ptr() if t[k] is not None else None  # noqa: E731
+        self._ana_struct = _abi.Analytics(p("heatmap"), p("coldmap"), p("launch"),
+                                          p("eng_log"), p("eng_count"), int(eng_cap),
+                                          p("ew_log"), p("ew_count"), int(ew_cap))
+        check(self.L.lnw_set_analytics(self.h, C.byref(self._ana_struct)))
+
+    def drain_analytics(self):
+        """Decoded records written since the last drain (numpy int64: see
+        analytics()), then both logs restart empty."""
+        an = self.analytics()
+        eng, ew = an["engagements"].cpu().numpy(), an["ew_fixes"].cpu().numpy()
+        self._ana["eng_count"].zero_()
+        self._ana["ew_count"].zero_()
+        return eng, ew
+
+    def disable_analytics(self):
+        check(self.L.lnw_set_analytics(self.h, None))
+        self._ana = None
+
+    def analytics(self):
+        """Decoded analytics: maps (device tensors) and the engagement / EW
+        records as int64 [n, 7] tensors (env, step, side, x1, y1, x2, y2) with
+        the missile count as an 8th engagement column; totals include records
+        past the capacity."""
+        t = self._ana
+        if t is None:
+            raise RuntimeError("analytics not enabled")
+
+        def recs(log, count, fix):
+            n = int(count.item())
+            r = log[: min(n, log.shape[0])].to(torch.int64) & 0xFFFFFFFF
+            w1, w2, w3 = r[:, 1], r[:, 2], r[:, 3]
+            cols = [r[:, 0], w1 & 0xFFFF, (w1 >> 16) & 0xFF, w2 & 0xFFFF, w2 >> 16]
+            if fix:  # int16 fix coordinates
+                cols += [((w3 & 0xFFFF) ^ 0x8000) - 0x8000, ((w3 >> 16) ^ 0x8000) - 0x8000]
+            else:
+                cols += [w3 & 0xFFFF, w3 >> 16, w1 >> 24]
+            return torch.stack(cols, 1), n
+
+        eng, n_eng = recs(t["eng_log"], t["eng_count"], False)
+        ew, n_ew = recs(t["ew_log"], t["ew_count"], True)
+        return dict(heatmap=t["heatmap"], coldmap=t["coldmap"], launch=t["launch"],
+                    engagements=eng, engagements_total=n_eng, ew_fixes=ew, ew_total=n_ew)
 
     def observe(self, agent=-1):
         """ship.get_obs() for every live ship (agent=-1, blue then red), one side

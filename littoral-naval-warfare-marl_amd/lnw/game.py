@@ -210,6 +210,7 @@ class Game:
             self._g = BatchedGame(1, [_NAMES[t] for t in types[:len(blue)]],
                                   [_NAMES[t] for t in types[len(blue):]], scenario=sc,
                                   device=self.device, grid=grid_arr)
+            self._g.enable_analytics(eng_cap=4096, ew_cap=4096, maps=False)
             self._key = key
         g = self._g
         g.set_rng(random.getrandbits(63))
@@ -247,8 +248,25 @@ class Game:
             self._tl_cache = self._g.tlists(0)
         return self._tl_cache
 
+    def _pull_analytics(self):
+        """Append the step's / observe's analytics records to the reference's
+        side channels: engagements, launch_sites, heatmap / coldmap (the side
+        being trained, combatant.py:640-657) and blue_ew / red_ew (:146-150)."""
+        eng, ew = self._g.drain_analytics()
+        trained = 0 if self.scenario.side == "blue" else 1
+        for _, _, side, sx, sy, tx, ty, msl in eng.tolist():
+            self.engagements.append(((sx, sy), (tx, ty), msl))
+            if msl > 0:
+                if side == trained:
+                    self.heatmap[sx, sy] += 1
+                    self.coldmap[tx, ty] += 1
+                self.launch_sites["blue" if side == 0 else "red"].append((sx, sy))
+        for _, _, side, ox, oy, fx, fy in ew.tolist():
+            (self.blue_ew if side == 0 else self.red_ew).append(((ox, oy), (fx, fy)))
+
     def _observe_one(self, a):
         ob, orr = self._g.observe(a)
+        self._pull_analytics()
         self._invalidate()
         nb = self._g.nb
         row = ob[0, a] if a < nb else orr[0, a - nb]
@@ -282,6 +300,7 @@ class Game:
             t = torch.from_numpy(buf).cuda(self.device)
             out = g.step(t, torch.from_numpy(kinds))
         torch.cuda.synchronize(self.device)
+        self._pull_analytics()
         after = t.cpu().numpy()[0]
         if not self.scenario.trained_red:                          # game.py:379 mutation
             for a in range(g.nb, A):

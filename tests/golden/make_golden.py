@@ -362,7 +362,7 @@ def _snapshot(env, ships_all, nb):
 def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_types,
                  spawn="ref", n_ep=4, steps=40, flags=None, dtype="f64",
                  act_lo=0.0, act_hi=1.0, observe=False, grid_id=0, seed=0,
-                 random_ls=0, mixed_rows=False):
+                 random_ls=0, mixed_rows=False, analytics=False):
     flags = dict(flags or {})
     F = dict(DISCRETE=False, LANDING_OPS=False, TACTICS="aggressive", SIDE="blue",
              TRAINED_RED=True, RED_AGGRESSION=0.4, N_RED_LANDINGSHIP=random_ls)
@@ -370,6 +370,8 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
     game.RED_AGGRESSION = F["RED_AGGRESSION"]
     game.N_RED_LANDINGSHIP = F["N_RED_LANDINGSHIP"]
     game.SIDE = F["SIDE"]
+    combatant.CUR_SIDE = F["SIDE"]  # the same config key (combatant.py:38, landingship.py:39)
+    landingship.CUR_SIDE = F["SIDE"]
     game.TRAINED_RED = F["TRAINED_RED"]
     game.DISCRETE = F["DISCRETE"]
     combatant.DISCRETE = F["DISCRETE"]
@@ -394,6 +396,9 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
                pre_obs_valid=[], pre_tl_cnt=[], pre_tl_xy=[], pre_tape_pos=[])
     ep_meta = []
     crashes = []
+    # analytics side channels (game.py:119-154, combatant.py:146-150, 640-657):
+    # engagement / EW records tagged with (episode, step), maps per episode
+    ana = dict(eng=[], ew=[], heat=[], cold=[], launch=[])
     try:
         for ep in range(n_ep):
             env = game.Game()
@@ -428,6 +433,18 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
                         tape_start=tape_start, nb=nb, nr=nr,
                         Db=env.observation_space, Dr=env.red_observation_space,
                         first_step=len(rec["done"]))
+            n_eng = n_bew = n_rew = 0
+
+            def ana_step(s):
+                nonlocal n_eng, n_bew, n_rew
+                for e in env.engagements[n_eng:]:
+                    (sx, sy), (tx, ty), msl = e
+                    ana["eng"].append((ep, s, sx, sy, tx, ty, int(msl)))
+                for side, lst, n0 in ((0, env.blue_ew, n_bew), (1, env.red_ew, n_rew)):
+                    for (ox, oy), (fx, fy) in lst[n0:]:
+                        ana["ew"].append((ep, s, side, ox, oy, int(fx), int(fy)))
+                n_eng, n_bew, n_rew = len(env.engagements), len(env.blue_ew), len(env.red_ew)
+
             for s in range(steps):
                 # ---- optional caller-side observe (main.py:280-333 pattern)
                 pre_obs = np.zeros((A, max(meta["Db"], meta["Dr"])), np.float32)
@@ -496,8 +513,18 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
                 rec["ep_index"].append(ep)
                 rec["victories"].append((env.blue_victory, env.red_victory))
                 rec["engagements"].append((env.blue_engagements, env.red_engagements))
+                if analytics:
+                    ana_step(s)
                 if cap["done"] == 0:
                     break
+            if analytics:
+                ana["heat"].append(np.array(env.heatmap, np.int32))
+                ana["cold"].append(np.array(env.coldmap, np.int32))
+                L = np.zeros((2, 100, 100), np.int32)
+                for k, side in enumerate(("blue", "red")):
+                    for (x, y) in env.launch_sites[side]:
+                        L[k, x, y] += 1
+                ana["launch"].append(L)
             meta["n_steps"] = len(rec["done"]) - meta["first_step"]
             meta["tape_end"] = len(tape.vals)
             ep_meta.append(meta)
@@ -541,6 +568,15 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
         ep_index=np.array(rec["ep_index"], np.int32),
         pre_tape_pos=np.array(rec["pre_tape_pos"], np.int32),
     )
+    if analytics:
+        n_ep_ok = len(ep_meta)
+        eng = [r for r in ana["eng"] if r[0] < n_ep_ok]
+        ew = [r for r in ana["ew"] if r[0] < n_ep_ok]
+        out.update(ana_eng=np.array(eng, np.int32).reshape(-1, 7),
+                   ana_ew=np.array(ew, np.int32).reshape(-1, 7),
+                   ana_heat=np.array(ana["heat"][:n_ep_ok], np.int32).reshape(-1, 100, 100),
+                   ana_cold=np.array(ana["cold"][:n_ep_ok], np.int32).reshape(-1, 100, 100),
+                   ana_launch=np.array(ana["launch"][:n_ep_ok], np.int32).reshape(-1, 2, 100, 100))
     if observe:
         out.update(pre_obs=np.array(rec["pre_obs"], np.float32),
                    pre_obs_valid=np.array(rec["pre_obs_valid"], np.uint8),
@@ -614,6 +650,20 @@ def main():
         make_astar(game, combatant, g100, g200, quick)
     if not only or "episodes" in only:
         make_episodes(game, combatant, landingship, grids, quick)
+    if "--analytics" in sys.argv or "analytics" in only:
+        make_analytics_episodes(game, combatant, landingship, grids, quick)
+
+
+def make_analytics_episodes(game, combatant, landingship, grids, quick):
+    """Episodes with the analytics side channels recorded."""
+    q = (lambda n: max(2, n // 3)) if quick else (lambda n: n)
+    S4, R4 = ["small"] * 4, ["large"] * 4
+    run_scenario(game, combatant, landingship, "ana_melee", grids, nb_types=S4, nr_types=R4,
+                 spawn="melee", n_ep=q(8), seed=21, analytics=True)
+    run_scenario(game, combatant, landingship, "ana_melee_red", grids, nb_types=S4, nr_types=R4,
+                 spawn="melee", n_ep=q(6), seed=22, analytics=True, flags=dict(SIDE="red"))
+    run_scenario(game, combatant, landingship, "ana_split_observe", grids, nb_types=S4,
+                 nr_types=R4, spawn="split", n_ep=q(6), seed=23, analytics=True, observe=True)
 
 
 if __name__ == "__main__":

@@ -83,3 +83,38 @@ def test_facade_default_reset_and_shapes(tmp_path, monkeypatch):
     obs, rew, done, cog = g.step([np.zeros(4, np.float32)] * 6)
     assert obs.shape == (1, 3, g.observation_space) and len(rew) == 3
     g.close()
+
+
+def test_facade_analytics_side_channels(tmp_path, monkeypatch):
+    """engagements / launch_sites / heatmap / coldmap / blue_ew / red_ew are
+    filled from the device analytics logs with the reference's relations:
+    every hit is an engagement (blue_/red_engagements count them), missile hits
+    are launch sites, the heatmap counts the trained side's missile hits."""
+    monkeypatch.chdir(tmp_path)
+    from lnw.game import Game, ShipSpec
+    random.seed(4)
+    np.random.seed(4)
+    g = Game()
+    g.scenario.landing_ops = False
+    g.scenario.n_red_landingship = 0
+    blue = [ShipSpec("blue", "small", p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
+    red = [ShipSpec("red", "large", p) for p in [(58, 55), (60, 60), (62, 52), (57, 64)]]
+    rng = np.random.default_rng(4)
+    for ep in range(6):
+        g.reset(4, 4, blue_ships=blue, red_ships=red)
+        for step in range(40):
+            for ship in g.blue_ships:
+                if ship is not None:
+                    ship.get_obs()
+            obs, rew, done, cog = g.step([rng.random(4).astype(np.float32) for _ in range(8)])
+            if done == 0:
+                break
+    # the engagement counters accumulate across resets, as the reference's do
+    assert len(g.engagements) == g.blue_engagements + g.red_engagements > 0
+    missile = [e for e in g.engagements if e[2] > 0]
+    assert len(g.launch_sites["blue"]) + len(g.launch_sites["red"]) == len(missile)
+    assert g.heatmap.sum() == len(g.launch_sites["blue"]) == g.coldmap.sum()
+    assert len(g.blue_ew) + len(g.red_ew) > 0
+    for (ox, oy), (fx, fy) in g.blue_ew + g.red_ew:
+        assert 0 <= ox < 100 and 0 <= oy < 100
+    g.close()

@@ -326,6 +326,39 @@ def test_episode_gpu_tape_march_astar(name, grids):
     _cmp_episode(name, grids, los_mode=1, move_mode=1)
 
 
+@pytest.mark.parametrize("name", ["ep_ana_melee.npz", "ep_ana_melee_red.npz",
+                                  "ep_ana_split_observe.npz"])
+def test_analytics_replay(name, grids):
+    """Analytics side channels (lnw_set_analytics) against the reference's
+    heatmap / coldmap / launch_sites / engagements / blue_ew / red_ew recorded
+    over the same tape-mode episodes (make_golden.py make_analytics_episodes)."""
+    from _gpu_replay import replay_gpu
+    fx = load_fixture(name)
+    n_steps = np.array([em["n_steps"] for em in episode_meta(fx)["episodes"]])
+    g = None
+    for kind, info, g, res in replay_gpu(fx, grids):
+        if kind == "reset":
+            g.enable_analytics(eng_cap=4096, ew_cap=4096)
+    torch.cuda.synchronize()
+    an = g.analytics()
+    assert an["engagements_total"] <= 4096 and an["ew_total"] <= 4096
+    np.testing.assert_array_equal(an["heatmap"].cpu().numpy(), fx["ana_heat"].sum(0))
+    np.testing.assert_array_equal(an["coldmap"].cpu().numpy(), fx["ana_cold"].sum(0))
+    np.testing.assert_array_equal(an["launch"].cpu().numpy(), fx["ana_launch"].sum(0))
+    eng = an["engagements"].cpu().numpy()
+    eng = eng[eng[:, 1] < n_steps[eng[:, 0]]]  # steps past an episode's end replay idle
+    got = sorted(tuple(int(v) for v in r[[0, 1, 3, 4, 5, 6, 7]]) for r in eng)
+    want = sorted(tuple(int(v) for v in r) for r in fx["ana_eng"])
+    assert got == want
+    ew = an["ew_fixes"].cpu().numpy()
+    ew = ew[ew[:, 1] < n_steps[ew[:, 0]]]
+    got = sorted(tuple(int(v) for v in r) for r in ew)
+    want = sorted(tuple(int(v) for v in r) for r in fx["ana_ew"])
+    assert got == want
+    g.disable_analytics()
+    g.close()
+
+
 def test_shard_invariance(grids):
     """Env sharding: two handles holding global envs [0,32) and [32,64) produce
     exactly the trajectories of one handle holding [0,64) (RNG keyed by global
