@@ -237,6 +237,17 @@ typedef struct lnw_analytics {
 } lnw_analytics;
 int lnw_set_analytics(lnw_handle *h, const lnw_analytics *a);
 
+/* ---- batched policy forward -------------------------
+ * The convolutional head and LayerNorm of the reference actor (network.py:70-85:
+ * conv 1->5, BatchNorm, ReLU, 2x2 max pool, conv 5->8, BatchNorm, ReLU, pool,
+ * linear 8->12, LayerNorm over [head, obs[49:]]) for B observation rows of
+ * obs_dim floats (the first 49 are the 7x7 window): out[B][n_in], n_in =
+ * obs_dim - 37 (<= 64). params: 578 + 2 n_in floats packed by
+ * lnw.rollout.BatchedActor.packed_features(). bn_running 0: per-row BatchNorm
+ * statistics (the reference's training-mode one-state calls), 1: running. */
+int lnw_actor_features(const float *params_dev, int32_t obs_dim, const float *obs_dev, int64_t B,
+                       int32_t bn_running, float *out_dev /* [B][n_in] */, void *stream);
+
 /* Host-side constants the kernels use (for tests): hit probability tables
  * 1-(1-p)^n for p in {0.45, 0.63}, n = 0..8, in float64 and float32. */
 int lnw_hit_tables(double *tab64 /* [2][9] */, float *tab32 /* [2][9] */);

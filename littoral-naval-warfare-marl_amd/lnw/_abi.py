@@ -25,7 +25,7 @@ SYMBOLS = [
     "lnw_abi_version", "lnw_last_error", "lnw_create", "lnw_destroy", "lnw_load_terrain",
     "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_state_field", "lnw_tlist_cap",
     "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
-    "lnw_fill_uniform_f32", "lnw_hit_tables", "lnw_set_analytics",
+    "lnw_fill_uniform_f32", "lnw_hit_tables", "lnw_set_analytics", "lnw_actor_features",
 ]
 
 
@@ -88,6 +88,7 @@ def load(path=None):
         "lnw_fill_uniform_f32": ([P, I64, U64, U64, P], C.c_int),
         "lnw_hit_tables": ([P, P], C.c_int),
         "lnw_set_analytics": ([P, P], C.c_int),
+        "lnw_actor_features": ([P, I32, P, I64, I32, P, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "liblnw.so")
-SOURCES = [os.path.join(CSRC, "lnw_kernels.hip")]
+SOURCES = [os.path.join(CSRC, "lnw_kernels.hip"), os.path.join(CSRC, "lnw_actor.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "lnw_device.h"), os.path.join(INCLUDE, "lnw.h")]
 
 

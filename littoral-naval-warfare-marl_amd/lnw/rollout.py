@@ -67,6 +67,38 @@ class BatchedActor(nn.Module):
         self.load_state_dict({k: v.reshape(self.state_dict()[k].shape) for k, v in sd.items()})
         return self
 
+    def packed_features(self):
+        """Parameters in lnw_actor_features' order (csrc/lnw_actor.hip): conv1
+        w, b; norm1 w, b, running mean, var; conv2 w, b; norm2 w, b, running
+        mean, var; convhead w, b; layernorm w, b (578 + 2 n_in floats)."""
+        parts = [self.conv1.weight, self.conv1.bias, self.norm1.weight, self.norm1.bias,
+                 self.norm1.running_mean, self.norm1.running_var, self.conv2.weight,
+                 self.conv2.bias, self.norm2.weight, self.norm2.bias, self.norm2.running_mean,
+                 self.norm2.running_var, self.convhead.weight, self.convhead.bias,
+                 self.layernorm.weight, self.layernorm.bias]
+        return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
+
+    def features(self, obs, bn="sample"):
+        """network.py:70-85 up to the LayerNorm -> [B, n_in]: the HIP kernel
+        for device tensors (lnw_actor_features), torch ops for host tensors."""
+        B = obs.shape[0]
+        if obs.is_cuda:
+            from . import _abi
+            L = _abi.load()
+            obs = obs.contiguous().float()
+            n_in = self.layernorm.normalized_shape[0]
+            out = torch.empty((B, n_in), dtype=torch.float32, device=obs.device)
+            params = self.packed_features()
+            _abi.check(L.lnw_actor_features(params.data_ptr(), obs.shape[1], obs.data_ptr(), B,
+                                            0 if bn == "sample" else 1, out.data_ptr(),
+                                            torch.cuda.current_stream(obs.device).cuda_stream))
+            return out
+        z = obs[:, :WINDOW].reshape(B, 1, 7, 7)
+        z = self.pool(F.relu(self._bn(self.norm1, self.conv1(z), bn)))
+        z = self.pool2(F.relu(self._bn(self.norm2, self.conv2(z), bn)))
+        z = self.convhead(torch.flatten(z, 1))
+        return self.layernorm(torch.cat((z, obs[:, WINDOW:]), 1))
+
     @staticmethod
     def _bn(m, z, bn):
         if bn == "sample":
@@ -75,12 +107,7 @@ class BatchedActor(nn.Module):
 
     def heads(self, obs, bn="sample"):
         """(normal mean, normal std) for every row of obs [B, D]."""
-        B = obs.shape[0]
-        z = obs[:, :WINDOW].reshape(B, 1, 7, 7)
-        z = self.pool(F.relu(self._bn(self.norm1, self.conv1(z), bn)))
-        z = self.pool2(F.relu(self._bn(self.norm2, self.conv2(z), bn)))
-        z = self.convhead(torch.flatten(z, 1))
-        x = self.layernorm(torch.cat((z, obs[:, WINDOW:]), 1))
+        x = self.features(obs, bn)
         x = torch.tanh(self.fc1(x))
         x = torch.tanh(self.fc2(x))
         x = torch.tanh(self.fc3(x))

@@ -89,3 +89,39 @@ def test_rollout_replays_with_stepped_actions():
         torch.testing.assert_close(o["rew_blue"], out["rewards"][:, t], rtol=0, atol=0)
     g1.close()
     g2.close()
+
+
+@pytest.mark.parametrize("bn", ["sample", "running"])
+def test_features_kernel_matches_torch(bn):
+    """lnw_actor_features (HIP conv head + LayerNorm) against the torch ops on
+    the same rows."""
+    from lnw.rollout import BatchedActor
+    torch.manual_seed(3)
+    a = BatchedActor.for_obs(68)
+    with torch.no_grad():  # non-trivial running statistics for the eval mode
+        a.norm1.running_mean.uniform_(-0.2, 0.2)
+        a.norm1.running_var.uniform_(0.5, 2.0)
+        a.norm2.running_mean.uniform_(-0.2, 0.2)
+        a.norm2.running_var.uniform_(0.5, 2.0)
+    obs = torch.rand(20000, 68)
+    obs[:, :49] = torch.randint(0, 256, (20000, 49)) / 255.0
+    with torch.no_grad():
+        want = a.features(obs, bn)
+        got = a.cuda().features(obs.cuda(), bn).cpu()
+    np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-4, atol=2e-5)
+
+
+def test_actor_device_matches_reference():
+    """The device actor (HIP conv head + batched GEMMs) against the reference
+    MLP's per-sample outputs (tests/golden/policy.npz)."""
+    from lnw.rollout import BatchedActor
+    gold = np.load(os.path.join(ROOT, "tests", "golden", "policy.npz"))
+    sd = {k[len("actor."):]: gold[k] for k in gold.files if k.startswith("actor.")}
+    a = BatchedActor.for_obs(gold["obs"].shape[1]).load_reference(sd).cuda()
+    obs, acts = torch.tensor(gold["obs"]).cuda(), torch.tensor(gold["acts"]).cuda()
+    with torch.no_grad():
+        mean, std = a.heads(obs, bn="sample")
+        lp, ent = a.get_dist(obs, acts, bn="sample")
+    np.testing.assert_allclose(mean.cpu().numpy(), gold["tr_mean"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(std.cpu().numpy(), gold["tr_std"], rtol=1e-5, atol=0)
+    np.testing.assert_allclose(lp.cpu().numpy(), gold["tr_lp"], rtol=0, atol=1e-4)
