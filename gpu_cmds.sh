@@ -1,7 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_rollout.py -q -x > gpurun_out/troll.log 2>&1; echo "rc=$?" >> gpurun_out/troll.log
-timeout -k 10 300 python tools/rollout_probe.py > gpurun_out/roll.log 2>&1 || exit 1
-export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_roll -o roll --output-format csv -- python3 tools/rollout_probe.py > gpurun_out/prof_roll.log 2>&1 || exit 1
-cp $(find /tmp/prof_roll -name "*kernel_stats.csv" | head -n 1) gpurun_out/roll_kernel_stats.csv
+timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/tgpu.log 2>&1 || { tail -30 gpurun_out/tgpu.log; exit 1; }
+tail -3 gpurun_out/tgpu.log
+timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 2
+cat gpurun_out/bench.json
+LNW_PROF=1 timeout -k 10 300 python bench.py --steps 3 --warmup 2 --no-cpu-baseline > /dev/null 2> gpurun_out/prof.err || exit 3
+grep "lnw prof" gpurun_out/prof.err | tail -2

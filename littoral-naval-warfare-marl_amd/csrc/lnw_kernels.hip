@@ -1241,13 +1241,14 @@ __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, c
 // ---------------------------------------------------------------------------
 // phase L: load state columns
 // ---------------------------------------------------------------------------
-template <int AT = 0>
+template <int AT, int NW>
 __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, int lane, int env,
-                                  bool valid) {
+                                  bool valid, int wid) {
   const long long E = P.E;
   const int A = AT > 0 ? AT : P.A;
 #pragma unroll
   for (int a = 0; a < (AT > 0 ? AT : A); a++) {
+    if (NW > 1 && a % NW != wid) continue;  // agents split across the waves
     size_t ai = (size_t)a * E + env;
     if (valid) {
       uint32_t p = S.pos[ai];
@@ -1407,17 +1408,20 @@ __device__ __forceinline__ void move_astar_pass(const KParams &P, const KState &
   }
 }
 
-template <int DT>
+// The NW waves of the workgroup take contiguous halves of the passes.
+template <int DT, int NW>
 __device__ __forceinline__ void move_phase(const KParams &P, const KState &S, Cols &c, const void *actions,
                                   const uint8_t *row_kind, const uint32_t *mask, int env0,
-                                  int nenv, int A) {
+                                  int nenv, int A, int wid) {
   // f32 (the rollout dtype) batches 8 passes; f64 / i32 go one pass at a time
   constexpr int B = DT == LNW_ACT_F32 ? 8 : 1;
   const int npass = (nenv * A + WAVE - 1) / WAVE;
+  const int share = (npass + NW - 1) / NW;
+  const int pbeg = wid * share, pend = pbeg + share < npass ? pbeg + share : npass;
 #pragma unroll 1
-  for (int p0 = 0; p0 < npass; p0 += B)
+  for (int p0 = pbeg; p0 < pend; p0 += B)
     move_batch_t<DT, B>(P, S, c, actions, row_kind, mask, env0, nenv, A, p0,
-                        npass - p0 < B ? npass - p0 : B);
+                        pend - p0 < B ? pend - p0 : B);
 }
 
 // diagnostics: per-workgroup phase timestamps (100 MHz real-time clock)
@@ -1463,33 +1467,45 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
   const bool emit = ST && P.los_mode == 0 && nenv == WAVE && !(P.dbg_skip & 3);
-  if (wid == 1) {
-    __syncthreads();
-    if constexpr (ST) {
-      if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
-    }
-    prof_stamp(S, 5);
-    return;
-  }
-  prof_stamp(S, 0);
+  // two-wave workgroups share phases L and M (agents / pair passes split);
+  // after M wave 1 turns to emission and wave 0 runs S
+  constexpr int NW = ST && EPW == WAVE ? 2 : 1;
+  if (NW == 1 && wid == 1) return;
+  if (wid == 0) prof_stamp(S, 0);
 
-  for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
+  for (int w = threadIdx.x; w < P.G * P.W16; w += NW * WAVE) c.mask[w] = S.mask2[w];
   const uint32_t *mask = c.mask;
-  load_state<NB + NR>(P, S, c, lane, env, valid);
+  load_state<NB + NR, NW>(P, S, c, lane, env, valid, wid);
   double duct = valid ? S.duct[env] : 1.0;
-  duct_col[lane] = duct;
-  if (lane == 0) prog = -1;
+  if (wid == 0) {
+    duct_col[lane] = duct;
+    if (lane == 0) prog = -1;
+  }
   __syncthreads();
-  prof_stamp(S, 4);
+  if (wid == 0) prof_stamp(S, 4);
 
   // ---- phase M: movement feasibility for every agent of this env --------
   // M1: load each action row once (a0/a1 kept in LDS for phase S) and compute
   //     the move target; M2: feasibility lookups (independent across agents).
   const int dt = P.act_dtype;
   if (!(P.dbg_skip & 4)) {
-    if (dt == LNW_ACT_F32) move_phase<LNW_ACT_F32>(P, S, c, actions, row_kind, mask, env0, nenv, A);
-    else if (dt == LNW_ACT_F64) move_phase<LNW_ACT_F64>(P, S, c, actions, row_kind, mask, env0, nenv, A);
-    else move_phase<LNW_ACT_I32>(P, S, c, actions, row_kind, mask, env0, nenv, A);
+    if (dt == LNW_ACT_F32)
+      move_phase<LNW_ACT_F32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
+    else if (dt == LNW_ACT_F64)
+      move_phase<LNW_ACT_F64, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
+    else
+      move_phase<LNW_ACT_I32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
+  }
+  if (NW > 1) __syncthreads();
+  if (wid == 1) {
+    if constexpr (ST) {
+      if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
+    }
+    prof_stamp(S, 5);
+    return;
+  }
+  if (!(P.dbg_skip & 4)) {
+    // the rare A* fallback (open lists sized for one wave)
     move_astar_pass(P, S, c, nenv, A);
     wave_lds_sync();
   }
@@ -1709,7 +1725,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   __shared__ double duct_col[WAVE];
   for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
   const uint32_t *mask = c.mask;
-  load_state(P, S, c, lane, env, valid);
+  load_state<0, 1>(P, S, c, lane, env, valid, 0);
   double duct = valid ? S.duct[env] : 1.0;
   duct_col[lane] = duct;
   __syncthreads();
