@@ -204,7 +204,7 @@ struct Rng {
     ctr++;
     return tape[p];
   }
-  __device__ double uniform() {
+  __device__ __forceinline__ double uniform() {
     if (mode == 1) return tnext();
     uint32_t o[4];
     block(o);

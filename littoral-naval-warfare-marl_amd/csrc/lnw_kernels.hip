@@ -166,18 +166,24 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
 #define COLW(arr, a) ((arr)[(a) * PAD + lane])
 #define COLB(arr, a) ((arr)[(a) * PADB + lane])
 
+// LNW_PROF diagnostics clock (100 MHz; 0 when profiling is off)
+__device__ inline unsigned long long prof_now(const KState &S) {
+  return S.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+}
+
 // Per-lane (per-env) context for phase S.
 struct Ctx {
   const KParams &P;
   const KState &S;
   Cols &c;
   int lane, env;
-  double duct;
+  const double *duct_col;  // per-env ducting factor in LDS (kept out of the registers)
   Rng rng;
   const uint32_t *mask;  // LDS (march mode) or global
   long long E;
   int r2max;             // max over ship-type pairs of radar^2, EW^2 and 16 (d < 4)
   int step;              // episode step being played (analytics records)
+  __device__ double duct() const { return duct_col[lane]; }
 };
 
 // analytics (lnw_set_analytics): one 4-word record appended to a capped log
@@ -264,7 +270,7 @@ __device__ inline void pair_detect(Ctx &X, int myradar, int i, int jj, int xi, i
   const KState &S = X.S;
   Cols &c = X.c;
   const int lane = X.lane;
-  int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
+  int rr = radar_r(P, X.duct(), ti, tj), re = ew_r(P, X.duct(), ti, tj);
   bool rad_ok = myradar == 1 && d2 < rr * rr;
   bool close = d2 < 16;
   bool ew_cand = d2 < re * re && radj == 1;
@@ -515,7 +521,7 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
       const int d2 = dx * dx + dy * dy;
       if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
       const int ti = COLB(c.type, i), tj = COLB(c.type, j);
-      const int rr = radar_r(P, X.duct, ti, tj), re = ew_r(P, X.duct, ti, tj);
+      const int rr = radar_r(P, X.duct(), ti, tj), re = ew_r(P, X.duct(), ti, tj);
       const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
       const bool ew_cand = d2 < re * re && COLW(c.radar_cur, j) == 1;
       if (!(rad_ok || close || ew_cand)) continue;  // LOS result would be unused
@@ -1425,9 +1431,6 @@ __device__ __forceinline__ void move_phase(const KParams &P, const KState &S, Co
 }
 
 // diagnostics: per-workgroup phase timestamps (100 MHz real-time clock)
-__device__ inline unsigned long long prof_now(const KState &S) {
-  return S.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
-}
 __device__ inline void prof_put(const KState &S, int slot, unsigned long long v) {
   if (S.prof && (threadIdx.x & (WAVE - 1)) == 0) S.prof[(size_t)blockIdx.x * 16 + slot] = v;
 }
@@ -1516,7 +1519,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   prof_stamp(S, 1);
   if (valid && !(P.dbg_skip & 2)) {
     if (emit) publish_progress(&prog, 0);
-    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), emit ? S.mask2 : mask, E,
+    Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), emit ? S.mask2 : mask, E,
           max_range2(P, duct), 0};
     Neut N{{0, 0}, {0u, 0u}};
     int ev[8];
@@ -1524,11 +1527,9 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     for (int q = 0; q < 8; q++) ev[q] = S.envi[q * E + env];
     X.step = ev[2];
     int hits[2] = {0, 0};
-    double bsx = 0, bsy = 0, rsx = 0, rsy = 0;
+    int bsx = 0, bsy = 0, rsx = 0, rsy = 0;  // exact integer sums
     int nbp = 0, nrp = 0;
-    unsigned long long pf_fire = 0, pf_obs = 0, pf_rest = 0;
     for (int a = 0; a < A; a++) {
-      unsigned long long pt0 = prof_now(S), pt1 = pt0, pt2 = pt0;
      do {
       if (!COLB(c.alive0, a)) { COLW(c.reward, a) = 0.0; break; }
       const int side = a >= nb;
@@ -1571,7 +1572,6 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
           if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
         }
       }
-      pt1 = prof_now(S);
       if (side) ev[6] += destroyed; else ev[5] += destroyed;
       if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
       else {
@@ -1587,7 +1587,6 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       } else {
         get_obs_dev(X, a);
       }
-      pt2 = prof_now(S);
       double r = reward_dev(X, a, moved, engage, destroyed);
       COLW(c.reward, a) = r;
       if (!side) {
@@ -1598,12 +1597,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       hits[side] += destroyed;
      } while (0);
       if (emit) publish_progress(&prog, a + 1);
-      const unsigned long long pt3 = prof_now(S);
-      pf_fire += pt1 - pt0; pf_obs += pt2 - pt1; pf_rest += pt3 - pt2;
     }
-    prof_put(S, 8, pf_fire);
-    prof_put(S, 9, pf_obs);
-    prof_put(S, 10, pf_rest);
     // ---- tail (game.py:409-520) -------------------------------------------
     int nbl = ev[0] - N.cnt[0];
     int nrl = ev[1] - N.cnt[1];
@@ -1669,7 +1663,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     int steps_env = ev[2] + 1;
     ev[2] = steps_env;
     if (nbp > 0 && nrp > 0) {
-      double bx = bsx / nbp, by = bsy / nbp, rx = rsx / nrp, ry = rsy / nrp;
+      double bx = (double)bsx / nbp, by = (double)bsy / nbp, rx = (double)rsx / nrp, ry = (double)rsy / nrp;
       cog = (float)sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
     }
     // outputs
@@ -1730,7 +1724,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   duct_col[lane] = duct;
   __syncthreads();
   if (valid) {
-    Ctx X{P, S, c, lane, env, duct, make_rng(P, S, env), mask, E, max_range2(P, duct),
+    Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), mask, E, max_range2(P, duct),
           S.envi[2 * E + env]};
     int a0 = 0, a1 = A;
     if (sel >= 0) { a0 = sel; a1 = sel + 1; }
@@ -2042,15 +2036,7 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
     if (r[0] < t0) t0 = r[0];
     if (r[3] > tend0) tend0 = r[3];
   }
-  double sf = 0, so = 0, sr = 0;
-  for (int w = 0; w < nwg; w++) {
-    sf += (double)t[(size_t)w * 16 + 8];
-    so += (double)t[(size_t)w * 16 + 9];
-    sr += (double)t[(size_t)w * 16 + 10];
-  }
   const double us = 0.01;  // 100 MHz ticks
-  fprintf(stderr, "[lnw prof] S split: engage %.2f us, get_obs %.2f us, reward+rest %.2f us\n",
-          sf / nwg * us, so / nwg * us, sr / nwg * us);
   fprintf(stderr, "[lnw prof] wg=%d mean L %.2f us, M %.2f us, S %.2f us, W %.2f us, wave1 end-from-start %.2f us; "
                   "grid: last wave0 end %.2f us, last wave1 end %.2f us after first start\n",
           nwg, sL / nwg * us, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
