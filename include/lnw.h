@@ -179,6 +179,13 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
 int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbytes);
 /* Target-list capacity T per agent (= max(nb,nr) + max(nb,nr)^2, never overflows). */
 int lnw_tlist_cap(lnw_handle *h);
+/* Environments per workgroup of the step / observe launches (build-side launch
+ * shape, no reference counterpart). epw = 0 restores the automatic choice made
+ * by lnw_load_terrain: 64 (one env per lane) unless E is too small to fill the
+ * GPU, then fewer per workgroup. 1 <= epw <= 64 forces it (results do not depend
+ * on it; tests use it to cover both launch shapes). Returns the epw in force, or
+ * a negative LNW_E* code. */
+int lnw_set_epw(lnw_handle *h, int32_t epw);
 
 /* ---- unit kernels (parity tests, standalone use) ------------------------ */
 /* LOS (radar thr = move_thr; EW thr): out[i] = bit0 radar clear | bit1 EW clear

@@ -51,6 +51,11 @@ struct LdsLayout {
   int stage;
   // terrain mask (phase M), aliased in phase S by the row-emission stage
   int mask, estage, total;
+  // quiet path (step_kernel, quiet_emit_t): per-wave row stages and the x/G LUT.
+  // qstage0 aliases the scratch that is dead once phase Q has run (actions,
+  // pos_new, observed lists); qstage1 the scratch dead after phase W (rewards,
+  // steps, missile kinds) plus the mask region; qlut sits at the very end.
+  int qstage0, qstage1, qlut;
 };
 
 // Row staging for phase O: up to 64 observation rows. The row stride S (floats)
@@ -80,6 +85,10 @@ __host__ __device__ inline int stage_bytes(int A, int nb, int nr, int G) {
 constexpr int EST4 = 5;
 __host__ __device__ inline int estage_bytes(int G) { return WAVE * EST4 * 16 + ((G + 3) & ~3) * 4; }
 
+// Quiet-path row stage: QEPG envs x one side's rows (stride stage_stride(ns)).
+constexpr int QEPG = 8;
+__host__ __device__ constexpr int qstage_bytes(int ns) { return QEPG * ns * stage_stride(ns) * 4; }
+
 __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax, int mask_words,
                                                 int G) {
   LdsLayout L;
@@ -97,21 +106,27 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   o = (o + 15) & ~15;
   const int scratch = o;
   L.stage = scratch;
-  L.pos_new = o; o += A * PAD * 4;
-  L.steps = o; o += A * PAD * 4;
-  o = (o + 7) & ~7;
-  // the A* open lists (phase M) alias the rewards (first written in phase S)
-  L.reward = o;
-  L.open = o;
-  o += (A * PAD * 8 > OPEN_CAP * EPW * 4) ? A * PAD * 8 : OPEN_CAP * EPW * 4;
+  // dead once phase Q (quiet path) or phase S has run
   L.act0 = o; o += A * PAD * 8;
   L.act1 = o; o += A * PAD * 8;
+  L.pos_new = o; o += A * PAD * 4;
   L.observed = o; o += nmax * PAD * 4;
-  L.mkind = o; o += A * PADB;
-  L.eng = o; o += A * PADB;
   L.bcnt = o; o += nmax * PADB;
   L.border = o; o += nmax * PADB;
   L.akind = o; o += A * PADB;
+  o = (o + 15) & ~15;
+  L.qstage0 = scratch;
+  const int qneed = qstage_bytes(nb > nr ? nb : nr);
+  if (o - scratch < qneed) o = scratch + qneed;
+  // dead once phase W has run; the A* open lists (phase M) alias the rewards
+  // (first written in phase Q / S)
+  L.qstage1 = o;
+  L.reward = o;
+  L.open = o;
+  o += (A * PAD * 8 > OPEN_CAP * EPW * 4) ? A * PAD * 8 : OPEN_CAP * EPW * 4;
+  L.steps = o; o += A * PAD * 4;
+  L.mkind = o; o += A * PADB;
+  L.eng = o; o += A * PADB;
   int st_end = scratch + stage_bytes(A, nb, nr, G);
   if (st_end > o) o = st_end;
   o = (o + 15) & ~15;
@@ -120,6 +135,9 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   // the emission stage exists only with full-wave workgroups (two-wave kernels)
   const int est = EPW == WAVE ? estage_bytes(G) : 0;
   o += mask_words * 4 > est ? mask_words * 4 : est;
+  const int lut = ((G + 3) & ~3) * 4;
+  if (o - L.qstage1 < qneed + lut) o = L.qstage1 + qneed + lut;
+  L.qlut = o - lut;
   L.total = o;
   return L;
 }
@@ -130,7 +148,7 @@ struct Cols {
   double *reward, *act0, *act1;
   uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border, *akind;
   uint32_t *mask;
-  float *stage, *estage;
+  float *stage, *estage, *qstage0, *qstage1, *qlut;
 };
 
 __device__ inline Cols carve(char *base, const LdsLayout &L) {
@@ -160,6 +178,9 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
   c.mask = (uint32_t *)(base + L.mask);
   c.stage = (float *)(base + L.stage);
   c.estage = (float *)(base + L.estage);
+  c.qstage0 = (float *)(base + L.qstage0);
+  c.qstage1 = (float *)(base + L.qstage1);
+  c.qlut = (float *)(base + L.qlut);
   return c;
 }
 
@@ -693,13 +714,11 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
   return hit;
 }
 
-// calculate_reward (game.py:214-295)
-__device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int n_hit) {
-  const KParams &P = X.P;
-  const KState &S = X.S;
-  Cols &c = X.c;
-  const int lane = X.lane;
-  size_t ai = (size_t)a * X.E + X.env;
+// calculate_reward (game.py:214-295) for agent a of the env in LDS column `lane`
+__device__ __forceinline__ double reward_core(const KParams &P, const KState &S, Cols &c, int lane,
+                                              long long E, int env, int a, bool moved, bool engage,
+                                              int n_hit) {
+  size_t ai = (size_t)a * E + env;
   int steps = COLW(c.steps, a) + 1;
   COLW(c.steps, a) = steps;
   int tl_n = (int)COLW(c.tcnt, a);
@@ -740,6 +759,10 @@ __device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int 
     else r += log10(100.0 / dl) * 5.0;
   }
   return r;
+}
+
+__device__ inline double reward_dev(Ctx &X, int a, bool moved, bool engage, int n_hit) {
+  return reward_core(X.P, X.S, X.c, X.lane, X.E, X.env, a, moved, engage, n_hit);
 }
 
 // Game.reset for one env (game.py:528-613), in-kernel
@@ -1021,7 +1044,7 @@ __device__ inline void row_regs_t(const Cols &c, const double *duct_col, int el,
   }
 }
 
-template <int NS, int NPASS4>
+template <int NS, int NPASS4, bool NT = true>
 __device__ inline void copy_side_t(const float *stage, float *out, float *dummy, int ne,
                                    long long genv0) {
   constexpr int D = 4 * NS + 52, D4 = D / 4, S4 = stage_stride(NS) / 4;
@@ -1043,7 +1066,8 @@ __device__ inline void copy_side_t(const float *stage, float *out, float *dummy,
   for (int u = 0; u < IT; u++) {  // unconditional stores: masked-out lanes hit the sink
     const int i = lane + u * WAVE;
     f32x4 *dst = i < n4 ? base + i : (f32x4 *)dummy + lane;
-    __builtin_nontemporal_store(v[u], dst);  // streamed out, not re-read by the kernel
+    if constexpr (NT) __builtin_nontemporal_store(v[u], dst);  // streamed out, not re-read
+    else *dst = v[u];
   }
 }
 
@@ -1439,6 +1463,119 @@ __device__ inline void prof_stamp(const KState &S, int slot) {
     S.prof[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Game.step tail (game.py:409-520) for the env in LDS column `lane` once every
+// agent has acted: team bonus, defensive loss penalty, victory / defeat,
+// landing-ops termination, episode counters, centre-of-gravity distance of the
+// pre-move positions, the per-env outputs, then phase W (state stored back, or
+// an in-kernel Game.reset when the episode ends).
+__device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols &c, int lane, int env,
+                                         int nb, int A, const Neut &N, int (&ev)[8],
+                                         const int (&hits)[2], int nbp, int nrp, int bsx, int bsy,
+                                         int rsx, int rsy, Rng &rng, float *rew_b, float *rew_r,
+                                         int32_t *done_out, float *cog_out) {
+  const long long E = P.E;
+  const int nr = A - nb;
+  int done = 1;
+  float cog = NAN;
+  // ---- tail (game.py:409-520) -------------------------------------------
+  int nbl = ev[0] - N.cnt[0];
+  int nrl = ev[1] - N.cnt[1];
+  ev[0] = nbl;
+  ev[1] = nrl;
+  bool no_blue = nbl == 0, no_red = nrl == 0;
+  for (int a = 0; a < A; a++) {
+    if (!COLB(c.alive0, a)) continue;
+    int side = a >= nb;
+    if (!COLB(c.eng, a)) COLW(c.reward, a) += (double)(hits[side] * 2);
+  }
+  if (!P.aggressive) {
+    for (int a = 0; a < A; a++) {
+      int side = a >= nb;
+      if (N.cnt[side] > 0) COLW(c.reward, a) = fmax(COLW(c.reward, a) - (double)(N.cnt[side] * 5), 0.0);
+    }
+  }
+  if (no_blue && !no_red) {
+    done = 0;
+    for (int a = 0; a < A; a++) {
+      if (a < nb) { if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a); }
+      else COLW(c.reward, a) += 100.0;
+    }
+    ev[4] += 1;
+  }
+  if (no_red && !no_blue) {
+    done = 0;
+    for (int a = 0; a < A; a++) {
+      if (a < nb) COLW(c.reward, a) += 100.0;
+      else if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
+    }
+    ev[3] += 1;
+  }
+  if (no_blue && no_red) {
+    done = 0;
+    for (int a = 0; a < A; a++) COLW(c.reward, a) += 10.0;
+  }
+  if (P.landing_ops) {
+    int rem = 0;
+    for (int a = nb; a < A; a++) rem += (COLB(c.alive0, a) && COLB(c.type, a) == T_LS) ? 1 : 0;
+    if (!rem) {
+      done = 0;
+      for (int a = 0; a < A; a++) {
+        if (a < nb) COLW(c.reward, a) += 100.0;
+        else COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
+      }
+      ev[3] += 1;
+    } else {
+      for (int l = nb; l < A; l++) {
+        if (!(COLB(c.alive0, l) && COLB(c.type, l) == T_LS)) continue;
+        uint32_t pl = COLW(c.pos_cur, l);
+        if (pos_x(pl) == P.lz_x && pos_y(pl) == P.lz_y) {
+          done = 0;
+          for (int a = 0; a < A; a++) {
+            if (a < nb) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
+            else COLW(c.reward, a) += 100.0;
+          }
+          ev[3] += 1;
+        }
+      }
+    }
+  }
+  int steps_env = ev[2] + 1;
+  ev[2] = steps_env;
+  if (nbp > 0 && nrp > 0) {
+    double bx = (double)bsx / nbp, by = (double)bsy / nbp, rx = (double)rsx / nrp, ry = (double)rsy / nrp;
+    cog = (float)sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
+  }
+  // outputs
+  for (int a = 0; a < nb; a++)
+    if (rew_b) rew_b[(size_t)env * nb + a] = (float)COLW(c.reward, a);
+  for (int a = 0; a < nr; a++)
+    if (rew_r) rew_r[(size_t)env * nr + a] = (float)COLW(c.reward, nb + a);
+  if (done_out) done_out[env] = done;
+  if (cog_out) cog_out[env] = cog;
+  prof_stamp(S, 2);
+  // ---- phase W: store state (alive updated by the neutralized lists) --
+  bool do_reset = P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
+  for (int a = 0; a < A; a++) {
+    size_t ai = (size_t)a * E + env;
+    int side = a >= nb;
+    bool killed = (N.mask[side] >> (a - (side ? nb : 0))) & 1u;
+    S.pos[ai] = COLW(c.pos_cur, a);
+    S.radar[ai] = COLW(c.radar_cur, a);
+    S.miss[ai] = COLB(c.miss_cur, a);
+    S.mkind[ai] = COLB(c.mkind, a);
+    S.alive[ai] = COLB(c.alive0, a) && !killed;
+    S.tl_cnt[ai] = (uint16_t)COLW(c.tcnt, a);
+    S.steps[ai] = COLW(c.steps, a);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
+  if (do_reset) reset_env_dev(P, S, env, rng);
+  S.rng[env] = rng.ctr;
+  if (rng.err) S.err[env] |= rng.err;
+}
+
+#include "lnw_quiet.inc"
+
 extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 
 // ---------------------------------------------------------------------------
@@ -1454,18 +1591,19 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = threadIdx.x / WAVE;
-  const int env0 = blockIdx.x * EPW;
+  const int epw = P.epw;
+  const int env0 = blockIdx.x * epw;
   const int env = env0 + lane;
   const long long E = P.E;
-  const bool valid = lane < EPW && env < E;
-  const int nenv = (E - env0) < EPW ? (int)(E - env0) : EPW;
+  const bool valid = lane < epw && env < E;
+  const int nenv = (E - env0) < epw ? (int)(E - env0) : epw;
   constexpr bool ST = NB > 0;
   const int nb = ST ? NB : P.nb, nr = ST ? NR : P.nr;
   const int A = nb + nr;
   LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
-  __shared__ int prog;
+  __shared__ int prog, qclaim;
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
@@ -1500,6 +1638,24 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       move_phase<LNW_ACT_I32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
   }
   if (NW > 1) __syncthreads();
+  // quiet workgroups (lnw_quiet.inc) skip phase S; deciding it needs the final
+  // moves, so wave 0 runs the A* fallback before a second barrier
+  const bool qcap = emit && P.trained_red && !(P.dbg_skip & 512);
+  if constexpr (ST && NW > 1) {
+    if (qcap) {
+      if (wid == 0) prof_stamp(S, 6);
+      if (wid == 0 && !(P.dbg_skip & 4)) move_astar_pass(P, S, c, nenv, A);
+      __syncthreads();
+      if (wid == 0) prof_stamp(S, 7);
+      const bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, duct_col[lane]));
+      if (wid == 0) prof_stamp(S, 8);
+      if (wq) {
+        quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, obs_b, obs_r, rew_b, rew_r,
+                             done_out, cog_out, env0);
+        return;
+      }
+    }
+  }
   if (wid == 1) {
     if constexpr (ST) {
       if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
@@ -1507,15 +1663,13 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     prof_stamp(S, 5);
     return;
   }
-  if (!(P.dbg_skip & 4)) {
+  if (!qcap && !(P.dbg_skip & 4)) {
     // the rare A* fallback (open lists sized for one wave)
     move_astar_pass(P, S, c, nenv, A);
     wave_lds_sync();
   }
 
   // ---- phase S: sequential agent loop ------------------------------------
-  int done = 1;
-  float cog = NAN;
   prof_stamp(S, 1);
   if (valid && !(P.dbg_skip & 2)) {
     if (emit) publish_progress(&prog, 0);
@@ -1581,13 +1735,14 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       uint32_t pn = COLW(c.pos_new, a);
       bool moved = (pn & 0x80000000u) != 0;
       if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
-      if constexpr (ST) {
+      if (P.dbg_skip & 128) {
+      } else if constexpr (ST) {
         if (!side) get_obs_t<NB, NR>(X, a, 0, NB);
         else get_obs_t<NR, NB>(X, a, NB, 0);
       } else {
         get_obs_dev(X, a);
       }
-      double r = reward_dev(X, a, moved, engage, destroyed);
+      double r = (P.dbg_skip & 256) ? 0.0 : reward_dev(X, a, moved, engage, destroyed);
       COLW(c.reward, a) = r;
       if (!side) {
         if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
@@ -1597,102 +1752,10 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       hits[side] += destroyed;
      } while (0);
       if (emit) publish_progress(&prog, a + 1);
+      if (a < 8) prof_stamp(S, 6 + a);
     }
-    // ---- tail (game.py:409-520) -------------------------------------------
-    int nbl = ev[0] - N.cnt[0];
-    int nrl = ev[1] - N.cnt[1];
-    ev[0] = nbl;
-    ev[1] = nrl;
-    bool no_blue = nbl == 0, no_red = nrl == 0;
-    for (int a = 0; a < A; a++) {
-      if (!COLB(c.alive0, a)) continue;
-      int side = a >= nb;
-      if (!COLB(c.eng, a)) COLW(c.reward, a) += (double)(hits[side] * 2);
-    }
-    if (!P.aggressive) {
-      for (int a = 0; a < A; a++) {
-        int side = a >= nb;
-        if (N.cnt[side] > 0) COLW(c.reward, a) = fmax(COLW(c.reward, a) - (double)(N.cnt[side] * 5), 0.0);
-      }
-    }
-    if (no_blue && !no_red) {
-      done = 0;
-      for (int a = 0; a < A; a++) {
-        if (a < nb) { if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a); }
-        else COLW(c.reward, a) += 100.0;
-      }
-      ev[4] += 1;
-    }
-    if (no_red && !no_blue) {
-      done = 0;
-      for (int a = 0; a < A; a++) {
-        if (a < nb) COLW(c.reward, a) += 100.0;
-        else if (!P.aggressive) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
-      }
-      ev[3] += 1;
-    }
-    if (no_blue && no_red) {
-      done = 0;
-      for (int a = 0; a < A; a++) COLW(c.reward, a) += 10.0;
-    }
-    if (P.landing_ops) {
-      int rem = 0;
-      for (int a = nb; a < A; a++) rem += (COLB(c.alive0, a) && COLB(c.type, a) == T_LS) ? 1 : 0;
-      if (!rem) {
-        done = 0;
-        for (int a = 0; a < A; a++) {
-          if (a < nb) COLW(c.reward, a) += 100.0;
-          else COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
-        }
-        ev[3] += 1;
-      } else {
-        for (int l = nb; l < A; l++) {
-          if (!(COLB(c.alive0, l) && COLB(c.type, l) == T_LS)) continue;
-          uint32_t pl = COLW(c.pos_cur, l);
-          if (pos_x(pl) == P.lz_x && pos_y(pl) == P.lz_y) {
-            done = 0;
-            for (int a = 0; a < A; a++) {
-              if (a < nb) COLW(c.reward, a) = COLW(c.reward, a) - COLW(c.reward, a);
-              else COLW(c.reward, a) += 100.0;
-            }
-            ev[3] += 1;
-          }
-        }
-      }
-    }
-    int steps_env = ev[2] + 1;
-    ev[2] = steps_env;
-    if (nbp > 0 && nrp > 0) {
-      double bx = (double)bsx / nbp, by = (double)bsy / nbp, rx = (double)rsx / nrp, ry = (double)rsy / nrp;
-      cog = (float)sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
-    }
-    // outputs
-    for (int a = 0; a < nb; a++)
-      if (rew_b) rew_b[(size_t)env * nb + a] = (float)COLW(c.reward, a);
-    for (int a = 0; a < nr; a++)
-      if (rew_r) rew_r[(size_t)env * nr + a] = (float)COLW(c.reward, nb + a);
-    if (done_out) done_out[env] = done;
-    if (cog_out) cog_out[env] = cog;
-    prof_stamp(S, 2);
-    // ---- phase W: store state (alive updated by the neutralized lists) --
-    bool do_reset = P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
-    for (int a = 0; a < A; a++) {
-      size_t ai = (size_t)a * E + env;
-      int side = a >= nb;
-      bool killed = (N.mask[side] >> (a - (side ? nb : 0))) & 1u;
-      S.pos[ai] = COLW(c.pos_cur, a);
-      S.radar[ai] = COLW(c.radar_cur, a);
-      S.miss[ai] = COLB(c.miss_cur, a);
-      S.mkind[ai] = COLB(c.mkind, a);
-      S.alive[ai] = COLB(c.alive0, a) && !killed;
-      S.tl_cnt[ai] = (uint16_t)COLW(c.tcnt, a);
-      S.steps[ai] = COLW(c.steps, a);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
-    if (do_reset) reset_env_dev(P, S, env, X.rng);
-    S.rng[env] = X.rng.ctr;
-    if (X.rng.err) S.err[env] |= X.rng.err;
+    env_tail(P, S, c, lane, env, nb, A, N, ev, hits, nbp, nrp, bsx, bsy, rsx, rsy, X.rng, rew_b,
+             rew_r, done_out, cog_out);
   }
   prof_stamp(S, 3);
   if ((P.dbg_skip & 1) || emit) return;
@@ -1708,11 +1771,12 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
 __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
                                                      float *obs_r) {
   const int lane = threadIdx.x & (WAVE - 1);
-  const int env0 = blockIdx.x * EPW;
+  const int epw = P.epw;
+  const int env0 = blockIdx.x * epw;
   const int env = env0 + lane;
   const long long E = P.E;
-  const bool valid = lane < EPW && env < E;
-  const int nenv = (E - env0) < EPW ? (int)(E - env0) : EPW;
+  const bool valid = lane < epw && env < E;
+  const int nenv = (E - env0) < epw ? (int)(E - env0) : epw;
   const int A = P.A, nb = P.nb;
   LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
@@ -2014,6 +2078,34 @@ size_t step_lds_bytes(const lnw_handle *h) {
   return (size_t)L.total;
 }
 
+// Environments per workgroup: EPW (one env per lane) unless that leaves the GPU
+// with fewer workgroups than it can hold at once; then halve it (down to 1) until
+// the grid fills every resident slot. A step is a per-lane latency chain, so a
+// workgroup with fewer live lanes takes about as long as a full one, and more
+// workgroups in flight finish the batch in fewer rounds (config 4: 8 192 envs
+// -> 512 workgroups of 16 instead of 128 of 64). LNW_EPW_RT overrides.
+int choose_epw(const lnw_handle *h) {
+  if (const char *e = getenv("LNW_EPW_RT")) {
+    int v = atoi(e);
+    if (v >= 1 && v <= EPW) return v;
+  }
+  int ncu = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
+    ncu = prop.multiProcessorCount;
+  const bool two_wave = !h->force_generic && h->nb == h->nr && h->nb >= 2 && h->nb <= 4 && EPW == WAVE;
+  const size_t lds = step_lds_bytes(h) + 1024;
+  int per_cu = (int)((160 * 1024) / lds);
+  const int by_waves = two_wave ? 4 : 8;  // 256 VGPRs: two waves per SIMD
+  if (per_cu > by_waves) per_cu = by_waves;
+  if (per_cu < 1) per_cu = 1;
+  const long long slots = (long long)ncu * per_cu;
+  int epw = EPW;
+  while (epw > 1 && (h->E + epw - 1) / epw < slots) epw /= 2;
+  if ((h->E + epw - 1) / epw > slots && epw < EPW) epw *= 2;  // never more rounds than EPW needs
+  return epw;
+}
+
 }  // namespace
 
 // LNW_PROF diagnostics: mean per-workgroup phase spans and the grid-wide
@@ -2023,7 +2115,8 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
   if (hipMemcpyAsync(t.data(), h->d_prof, t.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return;
-  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0;
+  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0, sa[8] = {0}, sq[4] = {0};
+  int nq = 0;
   unsigned long long t0 = ~0ull, tend0 = 0, tend1 = 0;
   int n1 = 0;
   for (int w = 0; w < nwg; w++) {
@@ -2033,6 +2126,16 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
     sS += (double)(r[2] - r[1]);
     sW += (double)(r[3] - r[2]);
     if (r[5]) { s1 += (double)(r[5] - r[0]); n1++; if (r[5] > tend1) tend1 = r[5]; }
+    if (r[9]) {  // quiet workgroup: M end | A* + barrier | predicate | phase Q + barrier
+      nq++;
+      sq[0] += (double)(r[6] - r[4]);
+      sq[1] += (double)(r[7] - r[6]);
+      sq[2] += (double)(r[8] - r[7]);
+      sq[3] += (double)(r[9] - r[8]);
+    } else {
+      for (int a = 0; a < 8; a++)
+        if (r[6 + a]) sa[a] += (double)(r[6 + a] - (a ? r[5 + a] : r[1]));
+    }
     if (r[0] < t0) t0 = r[0];
     if (r[3] > tend0) tend0 = r[3];
   }
@@ -2041,6 +2144,12 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
                   "grid: last wave0 end %.2f us, last wave1 end %.2f us after first start\n",
           nwg, sL / nwg * us, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
           (double)(tend0 - t0) * us, tend1 ? (double)(tend1 - t0) * us : 0.0);
+  if (nq)
+    fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us\n",
+            nq, sq[0] / nq * us, sq[1] / nq * us, sq[2] / nq * us, sq[3] / nq * us);
+  fprintf(stderr, "[lnw prof] phase S per agent (us):");
+  for (int a = 0; a < 8; a++) fprintf(stderr, " %.2f", sa[a] / nwg * us);
+  fprintf(stderr, "\n");
 }
 
 extern "C" {
@@ -2123,6 +2232,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   k.env_base = env_id_base;
   k.rng_mode = LNW_RNG_PHILOX;
   k.seed = 0;
+  k.epw = EPW;  // refined by lnw_load_terrain (choose_epw) once the LDS size is known
   host_constants(k);
   *out = h;
   return 0;
@@ -2211,6 +2321,7 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     }
   }
   (void)hipGetLastError();
+  h->kp.epw = choose_epw(h);
   return 0;
 }
 
@@ -2271,7 +2382,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   k.dbg_skip = h->dbg_skip;
   KState s = make_state(h);
   size_t lds = step_lds_bytes(h);
-  dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
+  dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
   if (h->prof) {
     if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * 16 * sizeof(unsigned long long)));
@@ -2299,7 +2410,7 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
   if (agent >= h->A || agent < LNW_OBS_RED) return fail(LNW_EINVAL, "bad agent selector");
   KState s = make_state(h);
   size_t lds = step_lds_bytes(h);
-  dim3 grid((h->E + EPW - 1) / EPW), block(WAVE);
+  dim3 grid((h->E + h->kp.epw - 1) / h->kp.epw), block(WAVE);
   observe_kernel<<<grid, block, lds, (hipStream_t)stream>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
   HIPCHK(hipGetLastError());
   return 0;
@@ -2329,6 +2440,14 @@ int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbyte
 }
 
 int lnw_tlist_cap(lnw_handle *h) { return h ? h->T : LNW_EINVAL; }
+
+int lnw_set_epw(lnw_handle *h, int32_t epw) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  if (epw < 0 || epw > EPW) return fail(LNW_EINVAL, "epw must be 0 (automatic) or 1..64");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  h->kp.epw = epw ? epw : choose_epw(h);
+  return h->kp.epw;
+}
 
 int lnw_los_batch(const uint8_t *grid_dev, int32_t G, const int16_t *pairs_dev, int64_t n,
                   int32_t move_thr, int32_t ew_thr, uint8_t *out_dev, void *stream) {

@@ -79,6 +79,7 @@ class BatchedGame:
         self.grid = np.ascontiguousarray(default_grid(100) if grid is None else grid, np.uint8)
         self.G = self.grid.shape[0]
         check(self.L.lnw_load_terrain(self.h, self.grid.ctypes.data_as(C.c_void_p), self.G))
+        self.epw = self.L.lnw_set_epw(self.h, 0)
         self._tape = None
         self.set_rng(seed)
         dev = self.device
@@ -100,6 +101,16 @@ class BatchedGame:
                         torch.int32: LNW_ACT_I32}
 
     # ---------------------------------------------------------------- rng
+    def set_epw(self, epw=0):
+        """Environments per workgroup of the step launch (lnw_set_epw): 0 = automatic
+        (64 unless E is too small to fill the GPU), 1..64 forces it. Returns the
+        value in force. Results do not depend on it."""
+        rc = self.L.lnw_set_epw(self.h, int(epw))
+        if rc < 0:
+            check(rc)
+        self.epw = rc
+        return rc
+
     def set_rng(self, seed):
         """Production RNG: Philox4x32-10 keyed by (seed, global env id)."""
         self._tape = None

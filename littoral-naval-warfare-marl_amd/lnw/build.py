@@ -15,7 +15,8 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "liblnw.so")
 SOURCES = [os.path.join(CSRC, "lnw_kernels.hip"), os.path.join(CSRC, "lnw_actor.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, "lnw_device.h"), os.path.join(INCLUDE, "lnw.h")]
+DEPS = SOURCES + [os.path.join(CSRC, "lnw_device.h"), os.path.join(CSRC, "lnw_quiet.inc"),
+                  os.path.join(INCLUDE, "lnw.h")]
 
 
 def hipcc():

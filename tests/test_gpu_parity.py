@@ -369,6 +369,7 @@ def test_shard_invariance(grids):
     box = ((40, 40), (57, 65))
     pos = [(6, 61), (10, 81), (8, 70), (11, 58), (98, 48), (98, 52), (98, 56), (96, 52)]
     full = BatchedGame(64, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=5)
+    assert full.set_epw(64) == 64  # one full two-wave workgroup: rows emitted during phase S
     parts = [BatchedGame(32, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=5,
                          env_id_base=b) for b in (0, 32)]
     for g in [full] + parts:
@@ -383,4 +384,160 @@ def test_shard_invariance(grids):
             merged = np.concatenate([op[0][k], op[1][k]])
             assert np.array_equal(of[k], merged, equal_nan=True), (s, k)
     for g in [full] + parts:
+        g.close()
+
+
+def _melee_positions(grid, E, nb, nr, seed, box_b=(30, 45, 40, 60), box_r=(55, 70, 45, 65)):
+    rng = np.random.default_rng(seed)
+    water = lambda x0, x1, y0, y1: [(x, y) for x in range(x0, x1) for y in range(y0, y1)
+                                    if grid[x, y] <= 74]
+    wb, wr = water(*box_b), water(*box_r)
+    return np.array([[wb[i] for i in rng.integers(0, len(wb), nb)] +
+                     [wr[i] for i in rng.integers(0, len(wr), nr)] for _ in range(E)], np.int32)
+
+
+@pytest.mark.parametrize("epw", [64, 16, 1])
+def test_philox_4v4_vs_oracle_launch_shapes(grids, epw):
+    """4v4 split spawns (fire, EW bearings and fixes happen) in production
+    (Philox) mode, 128 envs, with the step launched at 64 / 16 / 1 envs per
+    workgroup (64: the two-wave emission path; 16, 1: phase O after phase S),
+    every output bit-exact against the CPU oracle stepping the same envs."""
+    import _oracle
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    grid = grids[0]
+    E, S = 128, 10
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+                    grid=grid, seed=11)
+    assert g.set_epw(epw) == epw
+    pos = _melee_positions(grid, E, 4, 4, seed=epw)
+    g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
+    oracles = []
+    for e in range(E):
+        o = _oracle.OracleEnv(grid, 4, 4)
+        o.set_philox(11, e)
+        o.reset([0] * 4 + [1] * 4, pos[e])
+        oracles.append(o)
+    rng = np.random.default_rng(epw + 100)
+    for s in range(S):
+        act = rng.random((E, 8, 4)).astype(np.float32)
+        out = g.step(torch.from_numpy(act).cuda())
+        ob, orr = out["obs_blue"].cpu().numpy(), out["obs_red"].cpu().numpy()
+        rb, rr = out["rew_blue"].cpu().numpy(), out["rew_red"].cpu().numpy()
+        dn = out["done"].cpu().numpy()
+        for e in range(E):
+            r = oracles[e].step(act[e], np.full(8, _oracle.K_F32, np.int32))
+            assert np.array_equal(ob[e], r["obs_blue"].astype(np.float32)), (s, e, "obs_blue")
+            assert np.array_equal(orr[e], r["obs_red"].astype(np.float32)), (s, e, "obs_red")
+            assert np.allclose(rb[e], r["rew_blue"], rtol=0, atol=REW_TOL), (s, e, "rew_blue")
+            assert np.allclose(rr[e], r["rew_red"], rtol=0, atol=REW_TOL), (s, e, "rew_red")
+            assert dn[e] == r["done"], (s, e, "done")
+    g.close()
+
+
+def test_config4_launch_shape_invariance(grids):
+    """Config 4 shape (8 small blue vs 8 large + 2 LandingShip red, landing ops,
+    200x200 grid, box spawns): the automatic envs-per-workgroup choice, 64 and 1
+    give identical trajectories (observations, rewards, done, cog)."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    sc = Scenario(landing_ops=True, auto_reset=True, episode_steps=40)
+    E = 256
+    games = []
+    for epw in (0, 64, 1):
+        g = BatchedGame(E, ["small"] * 8, ["large"] * 8 + ["ls"] * 2, scenario=sc, grid=grids[1],
+                        seed=3)
+        g.set_epw(epw)
+        g.reset(positions=[(0, 0)] * 18, rand_ls=[0] * 16 + [1, 1], box=((20, 60), (80, 140)))
+        games.append(g)
+    assert games[0].epw < 64  # 256 envs cannot fill the GPU at 64 per workgroup
+    rng = np.random.default_rng(1)
+    for s in range(50):
+        act = torch.from_numpy(rng.random((E, 18, 4)).astype(np.float32)).cuda()
+        outs = [{k: v.cpu().numpy().copy() for k, v in g.step(act.clone()).items()} for g in games]
+        for o in outs[1:]:
+            for k in outs[0]:
+                assert np.array_equal(outs[0][k], o[k], equal_nan=True), (s, k)
+    for g in games:
+        g.close()
+
+
+REF_SPAWNS = [(6, 61), (10, 81), (8, 70), (11, 58), (98, 48), (98, 52), (98, 56), (96, 52)]
+
+
+def test_quiet_path_vs_oracle(grids):
+    """Quiet workgroups (lnw_quiet.inc): 128 envs at 64 per workgroup in Philox
+    mode; workgroup 0 holds reference spawns (quiet: no sensor contact, phase Q
+    + whole-block emission), workgroup 1 half reference, half split spawns (not
+    quiet: phase S). Every output bit-exact against the CPU oracle."""
+    import _oracle
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    grid = grids[0]
+    E, S = 128, 14
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+                    grid=grid, seed=21)
+    assert g.set_epw(64) == 64
+    pos = np.array([REF_SPAWNS] * E, np.int32)
+    pos[96:] = _melee_positions(grid, 32, 4, 4, seed=4)
+    g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
+    oracles = []
+    for e in range(E):
+        o = _oracle.OracleEnv(grid, 4, 4)
+        o.set_philox(21, e)
+        o.reset([0] * 4 + [1] * 4, pos[e])
+        oracles.append(o)
+    rng = np.random.default_rng(8)
+    for s in range(S):
+        act = rng.random((E, 8, 4)).astype(np.float32)
+        out = g.step(torch.from_numpy(act).cuda())
+        ob, orr = out["obs_blue"].cpu().numpy(), out["obs_red"].cpu().numpy()
+        rb, rr = out["rew_blue"].cpu().numpy(), out["rew_red"].cpu().numpy()
+        dn, cg = out["done"].cpu().numpy(), out["cog"].cpu().numpy()
+        for e in range(E):
+            r = oracles[e].step(act[e], np.full(8, _oracle.K_F32, np.int32))
+            assert np.array_equal(ob[e], r["obs_blue"].astype(np.float32)), (s, e, "obs_blue")
+            assert np.array_equal(orr[e], r["obs_red"].astype(np.float32)), (s, e, "obs_red")
+            assert np.allclose(rb[e], r["rew_blue"], rtol=0, atol=REW_TOL), (s, e, "rew_blue")
+            assert np.allclose(rr[e], r["rew_red"], rtol=0, atol=REW_TOL), (s, e, "rew_red")
+            assert dn[e] == r["done"], (s, e, "done")
+            assert abs(cg[e] - r["cog"]) <= 1e-5 or (np.isnan(cg[e]) and np.isnan(r["cog"])), (s, e)
+    g.close()
+
+
+@pytest.mark.parametrize("spawns", ["reference", "mixed"])
+def test_quiet_path_vs_phase_s_long(grids, spawns):
+    """The bench workload shape (auto-reset, 40-step episodes, Philox) over 90
+    steps: 64 envs per workgroup (quiet path where it applies) against 16 per
+    workgroup (phase S + phase O everywhere): identical observations, rewards,
+    done, cog and final state. "mixed": workgroups 1 and 3 spawn (and re-spawn)
+    in the melee box, 0 and 2 at the reference spawns."""
+    from lnw import _abi
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40)
+    E = 256
+    pos = np.array([REF_SPAWNS] * E, np.int32)
+    if spawns == "mixed":
+        for w in (1, 3):
+            pos[64 * w:64 * (w + 1)] = _melee_positions(grids[0], 64, 4, 4, seed=w)
+    games = []
+    for epw in (64, 16):
+        g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=9)
+        assert g.set_epw(epw) == epw
+        g.reset(positions=REF_SPAWNS, pos_per_env=torch.from_numpy(pos))
+        games.append(g)
+    rng = np.random.default_rng(2)
+    for s in range(90):
+        act = torch.from_numpy(rng.random((E, 8, 4)).astype(np.float32)).cuda()
+        outs = [{k: v.cpu().numpy().copy() for k, v in g.step(act.clone()).items()} for g in games]
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), (s, k)
+    sts = [g.env_state() for g in games]
+    for k in sts[0]:
+        assert np.array_equal(sts[0][k], sts[1][k], equal_nan=True), k
+    for f in range(_abi.F_TL):  # per-agent fields (target-list contents: via counts)
+        a, b = (g.get(f).cpu().numpy() for g in games)
+        assert np.array_equal(a, b, equal_nan=True), f
+    for g in games:
         g.close()
