@@ -1313,7 +1313,7 @@ __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, in
 // loads of one batch are issued before any is used.
 // ---------------------------------------------------------------------------
 template <int DT, int MAXP>
-__device__ __forceinline__ void move_batch_t(const KParams &P, const KState &S, Cols &c, const void *actions,
+__device__ __forceinline__ bool move_batch_t(const KParams &P, const KState &S, Cols &c, const void *actions,
                              const uint8_t *row_kind, const uint32_t *mask, int env0, int nenv,
                              int A, int p0, int np) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1398,6 +1398,7 @@ __device__ __forceinline__ void move_batch_t(const KParams &P, const KState &S, 
     }
   }
   uint32_t w[MAXP];
+  bool pend = false;
 #pragma unroll
   for (int k = 0; k < MAXP; k++) {
     if (k >= np) break;
@@ -1411,11 +1412,13 @@ __device__ __forceinline__ void move_batch_t(const KParams &P, const KState &S, 
     if (q >= npair || !(tg[k] & 0x40000000u)) continue;  // pos_new stays p (load_state)
     if (mw[k] < 0) {  // outside the table: left flagged for the A* pass below
       c.pos_new[a * PAD + e] = tg[k];
+      pend = true;
       continue;
     }
     const bool feas = (w[k] >> (mw[k] & 31)) & 1u;
     c.pos_new[a * PAD + e] = feas ? ((tg[k] & 0x3fffffffu) | 0x80000000u) : c.pos_old[a * PAD + e];
   }
+  return pend;
 }
 
 // check_path by A* for the candidates the table did not cover (still flagged
@@ -1440,7 +1443,7 @@ __device__ __forceinline__ void move_astar_pass(const KParams &P, const KState &
 
 // The NW waves of the workgroup take contiguous halves of the passes.
 template <int DT, int NW>
-__device__ __forceinline__ void move_phase(const KParams &P, const KState &S, Cols &c, const void *actions,
+__device__ __forceinline__ bool move_phase(const KParams &P, const KState &S, Cols &c, const void *actions,
                                   const uint8_t *row_kind, const uint32_t *mask, int env0,
                                   int nenv, int A, int wid) {
   // f32 (the rollout dtype) batches 8 passes; f64 / i32 go one pass at a time
@@ -1448,10 +1451,12 @@ __device__ __forceinline__ void move_phase(const KParams &P, const KState &S, Co
   const int npass = (nenv * A + WAVE - 1) / WAVE;
   const int share = (npass + NW - 1) / NW;
   const int pbeg = wid * share, pend = pbeg + share < npass ? pbeg + share : npass;
+  bool pending = false;  // this lane left a candidate for the A* pass
 #pragma unroll 1
   for (int p0 = pbeg; p0 < pend; p0 += B)
-    move_batch_t<DT, B>(P, S, c, actions, row_kind, mask, env0, nenv, A, p0,
-                        pend - p0 < B ? pend - p0 : B);
+    pending |= move_batch_t<DT, B>(P, S, c, actions, row_kind, mask, env0, nenv, A, p0,
+                                   pend - p0 < B ? pend - p0 : B);
+  return pending;
 }
 
 // diagnostics: per-workgroup phase timestamps (100 MHz real-time clock)
@@ -1604,6 +1609,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
   __shared__ int prog, qclaim;
+  __shared__ int r2col[WAVE];  // per-env max sensor reach^2 (max_range2)
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
@@ -1620,6 +1626,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   double duct = valid ? S.duct[env] : 1.0;
   if (wid == 0) {
     duct_col[lane] = duct;
+    r2col[lane] = max_range2(P, duct);
     if (lane == 0) prog = -1;
   }
   __syncthreads();
@@ -1629,25 +1636,29 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // M1: load each action row once (a0/a1 kept in LDS for phase S) and compute
   //     the move target; M2: feasibility lookups (independent across agents).
   const int dt = P.act_dtype;
+  bool pend = false;
   if (!(P.dbg_skip & 4)) {
     if (dt == LNW_ACT_F32)
-      move_phase<LNW_ACT_F32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
+      pend = move_phase<LNW_ACT_F32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
     else if (dt == LNW_ACT_F64)
-      move_phase<LNW_ACT_F64, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
+      pend = move_phase<LNW_ACT_F64, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
     else
-      move_phase<LNW_ACT_I32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
+      pend = move_phase<LNW_ACT_I32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
   }
-  if (NW > 1) __syncthreads();
+  // workgroup-wide: did any pair leave the move table's window (A* pass needed)?
+  const bool astar = NW > 1 ? __syncthreads_or(pend) != 0 : true;
   // quiet workgroups (lnw_quiet.inc) skip phase S; deciding it needs the final
   // moves, so wave 0 runs the A* fallback before a second barrier
   const bool qcap = emit && P.trained_red && !(P.dbg_skip & 512);
   if constexpr (ST && NW > 1) {
     if (qcap) {
       if (wid == 0) prof_stamp(S, 6);
-      if (wid == 0 && !(P.dbg_skip & 4)) move_astar_pass(P, S, c, nenv, A);
-      __syncthreads();
+      if (astar) {
+        if (wid == 0) move_astar_pass(P, S, c, nenv, A);
+        __syncthreads();
+      }
       if (wid == 0) prof_stamp(S, 7);
-      const bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, duct_col[lane]));
+      const bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
       if (wid == 0) prof_stamp(S, 8);
       if (wq) {
         quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, obs_b, obs_r, rew_b, rew_r,
@@ -1663,7 +1674,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     prof_stamp(S, 5);
     return;
   }
-  if (!qcap && !(P.dbg_skip & 4)) {
+  if (!qcap && astar && !(P.dbg_skip & 4)) {
     // the rare A* fallback (open lists sized for one wave)
     move_astar_pass(P, S, c, nenv, A);
     wave_lds_sync();
@@ -1674,7 +1685,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   if (valid && !(P.dbg_skip & 2)) {
     if (emit) publish_progress(&prog, 0);
     Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), emit ? S.mask2 : mask, E,
-          max_range2(P, duct), 0};
+          r2col[lane], 0};
     Neut N{{0, 0}, {0u, 0u}};
     int ev[8];
 #pragma unroll
