@@ -1268,6 +1268,30 @@ __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, c
   }
 }
 
+// The 2-bit terrain mask into LDS: 16-B loads, all of a thread's issued before
+// any is stored (a plain word loop waits out one L2 round trip per word).
+template <int NW>
+__device__ __forceinline__ void stage_mask(const KParams &P, const KState &S, uint32_t *dst) {
+  const int nw = P.G * P.W16, n4 = nw >> 2;
+  const uint4 *src4 = (const uint4 *)S.mask2;
+  uint4 *dst4 = (uint4 *)dst;
+  constexpr int U = 4;
+  for (int i0 = threadIdx.x; i0 < n4; i0 += U * NW * WAVE) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int i = i0 + u * NW * WAVE;
+      if (i < n4) v[u] = src4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int i = i0 + u * NW * WAVE;
+      if (i < n4) dst4[i] = v[u];
+    }
+  }
+  for (int w = (n4 << 2) + (int)threadIdx.x; w < nw; w += NW * WAVE) dst[w] = S.mask2[w];
+}
+
 // ---------------------------------------------------------------------------
 // phase L: load state columns
 // ---------------------------------------------------------------------------
@@ -1620,7 +1644,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   if (NW == 1 && wid == 1) return;
   if (wid == 0) prof_stamp(S, 0);
 
-  for (int w = threadIdx.x; w < P.G * P.W16; w += NW * WAVE) c.mask[w] = S.mask2[w];
+  stage_mask<NW>(P, S, c.mask);
   const uint32_t *mask = c.mask;
   load_state<NB + NR, NW>(P, S, c, lane, env, valid, wid);
   double duct = valid ? S.duct[env] : 1.0;
