@@ -260,7 +260,7 @@ def main():
         E, rank, world, args, args.spawns, args.los_mode, args.move_mode, args.steps, args.warmup, cfg)
     elapsed, kms_mean = dist.reduce_max([elapsed, kms_mean])
     value = world * E * args.steps / elapsed
-    nb = nr = 4
+    nb, nr = (len(cfg["blue"]), len(cfg["red"])) if cfg else (4, 4)
     B = algorithmic_bytes(nb, nr)
     achieved = B * E / (kms_mean * 1e-3) / 1e9
     traffic = None
@@ -296,7 +296,8 @@ def main():
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         line = {
-            "metric": "env-steps/sec (whole node), 65536 parallel 4v4 envs on 100x100 grid",
+            "metric": "env-steps/sec (whole node), 65536 parallel 4v4 envs on 100x100 grid"
+                      if cfg is None else "env-steps/sec, config 4 (diagnostic line)",
             "value": value,
             "unit": "env-steps/sec",
             "n_gpus": world,
@@ -309,11 +310,17 @@ def main():
             "dtype": "f64+i32",
             "data": "synthetic",
             "config": {
-                "workload": f"{E} parallel 4v4 envs per GPU, 100x100 Baltic grid, "
-                            f"{args.spawns} spawns, 40-step episodes with auto-reset, "
-                            "U[0,1)^4 f32 actions",
-                "envs_per_gpu": E, "global_envs": world * E, "agents": "4v4",
-                "grid": 100, "spawns": args.spawns, "los_mode": args.los_mode,
+                "workload": (f"{E} parallel 4v4 envs per GPU, 100x100 Baltic grid, "
+                             f"{args.spawns} spawns, 40-step episodes with auto-reset, "
+                             "U[0,1)^4 f32 actions") if cfg is None else
+                            (f"{E} parallel 8v8+2LS envs per GPU (config 4), 200x200 grid, "
+                             "box spawns, landing ops, 40-step episodes with auto-reset, "
+                             "U[0,1)^4 f32 actions"),
+                "envs_per_gpu": E, "global_envs": world * E,
+                "agents": "4v4" if cfg is None else f"{nb}v{nr}",
+                "grid": 100 if cfg is None else cfg["G"],
+                "spawns": args.spawns if cfg is None else "box",
+                "los_mode": args.los_mode,
                 "move_mode": args.move_mode, "parallelism": f"env-shard x{world}",
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
