@@ -47,7 +47,7 @@ struct KParams {
   double det_q[2];    // detected_prob: [0] target radar==1 (0.345-0.1), [1] otherwise
   int box_lo[2], box_hi[2];
   int epw;            // environments per workgroup (<= EPW; fewer when E is small, to fill the CUs)
-  int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission
+  int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch
 };
 
 // Device state (SoA, agent-major [field][agent][env] so a wave of envs reads
@@ -69,6 +69,7 @@ struct KState {
   uint32_t *err;       // [E]
   double *bear_val;    // [nmax*nmax][E] EW bearing scratch
   uint8_t *bear_ship;  // [nmax*nmax][E]
+  const double *atan_deg;  // [LOS_W][LOS_W] degrees(atan2(dy, dx)), host libm (EW bearings)
   const uint8_t *grid;     // [G][G]
   const float *gridf;      // [G][G] grid/255 as float32
   const float *winf;       // [2][G*G][52] Combatant | LandingShip observation windows
@@ -215,6 +216,18 @@ struct Rng {
     if (mode == 1) return tnext();
     uint32_t o[4];
     block(o);
+    double a = u53(o[0], o[1]), b = u53(o[2], o[3]);
+    return sqrt(-2.0 * p_log(1.0 - a)) * p_cos2pi(b);
+  }
+  // the gauss draw with draw number c (Philox counter / tape position), without
+  // touching the cursor: deferred bearings (finish_obs_t)
+  __device__ double gauss_at(unsigned long long c) const {
+    if (mode == 1) {
+      const long long p = tape_lo + (long long)c;
+      return p < tape_hi ? tape[p] : 0.0;
+    }
+    uint32_t o[4] = {(uint32_t)c, (uint32_t)(c >> 32), g0, g1};
+    philox10(o, k0, k1);
     double a = u53(o[0], o[1]), b = u53(o[2], o[3]);
     return sqrt(-2.0 * p_log(1.0 - a)) * p_cos2pi(b);
   }

@@ -188,8 +188,19 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
 #define COLB(arr, a) ((arr)[(a) * PADB + lane])
 
 // LNW_PROF diagnostics clock (100 MHz; 0 when profiling is off)
+constexpr int PROF_SLOTS = 32;  // per-workgroup record (slot map at prof_put)
 __device__ inline unsigned long long prof_now(const KState &S) {
   return S.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+}
+// adds the time since t0 to a workgroup slot from the first active lane (the
+// wave-level span of a section entered by only some lanes); returns now
+__device__ inline unsigned long long prof_acc(const KState &S, int slot, unsigned long long t0) {
+  if (!S.prof) return 0ull;
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long m = __ballot(1);
+  if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1)
+    atomicAdd(&S.prof[(size_t)blockIdx.x * PROF_SLOTS + slot], t - t0);
+  return t;
 }
 
 // Per-lane (per-env) context for phase S.
@@ -204,6 +215,11 @@ struct Ctx {
   long long E;
   int r2max;             // max over ship-type pairs of radar^2, EW^2 and 16 (d < 4)
   int step;              // episode step being played (analytics records)
+  // LOS bits of every (own ship, opponent) pair get_obs can query during this
+  // step (los_prefetch_t), per side: bit ((i*NOPP + j)*2 + v)*2 -> radar, +1 -> EW,
+  // v = own ship i at its new cell. Valid when `pre` is set.
+  uint64_t lpre[2];
+  bool pre;
   __device__ double duct() const { return duct_col[lane]; }
 };
 
@@ -300,14 +316,14 @@ __device__ inline void pair_detect(Ctx &X, int myradar, int i, int jj, int xi, i
                  los_q(P, S, X.mask, xi, yi, xj, yj), acc);
 }
 
-// The LOS-dependent part of one get_obs pair (combatant.py:106-124).
-__device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int xj, int yj,
-                                      bool rad_ok, bool close, bool ew_cand, uint32_t los,
-                                      ObsAcc &acc) {
-  const KState &S = X.S;
+// The observed-list part of one get_obs pair (combatant.py:106-118): radar or
+// close detection through a clear radar LOS, de-duplicated by position.
+// Returns true when the pair yields an EW bearing (combatant.py:119-124).
+__device__ inline bool pair_observe(Ctx &X, int xj, int yj, bool rad_ok, bool close, bool ew_cand,
+                                    uint32_t los, ObsAcc &acc) {
   Cols &c = X.c;
   const int lane = X.lane;
-  if (!(los & 1u)) return;
+  if (!(los & 1u)) return false;
   uint32_t pk = pack_pos(xj, yj);
   bool seen = false;
   for (int q = 0; q < acc.obs_n; q++) seen |= COLW(c.observed, q) == pk;
@@ -316,14 +332,28 @@ __device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int
     acc.obs_n++;
     seen = true;
   }
-  if (ew_cand && (los & 2u) && !seen) {
-    // calculate_bearing (combatant.py:249-263)
-    double bearing = atan2((double)(yj - yi), (double)(xj - xi)) * RAD2DEG;
-    double distortion = X.rng.gauss();
-    if (bearing + distortion < 0)
-      bearing = bearing + distortion + 360.0;
-    else
-      bearing = bearing + distortion;
+  return ew_cand && (los & 2u) && !seen;
+}
+
+// calculate_bearing (combatant.py:249-263) with the gauss draw given
+__device__ inline double ew_bearing(int xi, int yi, int xj, int yj, double distortion) {
+  double bearing = atan2((double)(yj - yi), (double)(xj - xi)) * RAD2DEG;
+  if (bearing + distortion < 0)
+    bearing = bearing + distortion + 360.0;
+  else
+    bearing = bearing + distortion;
+  return bearing;
+}
+
+// The LOS-dependent part of one get_obs pair (combatant.py:106-124).
+__device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int xj, int yj,
+                                      bool rad_ok, bool close, bool ew_cand, uint32_t los,
+                                      ObsAcc &acc) {
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  if (pair_observe(X, xj, yj, rad_ok, close, ew_cand, los, acc)) {
+    const double bearing = ew_bearing(xi, yi, xj, yj, X.rng.gauss());
     int k = COLB(c.bcnt, jj);
     if (k == 0) { COLB(c.border, acc.norder) = (uint8_t)jj; acc.norder++; }
     size_t slot = (size_t)(jj * S.nmax + k) * X.E + X.env;
@@ -580,9 +610,163 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   finish_obs<16, false>(X, me, opp0, opp1, acc);
 }
 
+// Select a[k] of a small register array without indexing (which would move
+// the array to scratch).
+template <int N, class T>
+__device__ __forceinline__ T rsel(const T (&a)[N], int k) {
+  T v = a[0];
+#pragma unroll
+  for (int q = 1; q < N; q++) v = k == q ? a[q] : v;
+  return v;
+}
+
+// Target list of a templated get_obs (combatant.py:128-161) from pass 1's
+// observed list and bearing requests. Bearing k of the call (pair
+// order) takes gauss draw base+k; the draws of opponents with a single bearing
+// are consumed but never evaluated (Philox and the tape are indexed by draw
+// number). Per opponent j the bearings come from own ships i ascending, i.e. in
+// the order the reference appends them, so consecutive-pair fixes stream
+// without storage; the mean of m = n-1 <= 3 fixes is a plain left-to-right sum
+// (np.mean below 8 terms). Fix targets are appended in the order of each
+// opponent's first bearing.
+template <int NOWN, int NOPP>
+__device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const ObsAcc &acc,
+                                    uint32_t bearm) {
+  static_assert(NOWN < 9, "np.mean pairwise summation starts at 8 terms");
+  const KParams &P = X.P;
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const long long E = X.E;
+  const int env = X.env;
+  const unsigned long long base = X.rng.ctr;
+  const int nbear = __builtin_popcount(bearm);
+  if (X.rng.mode == 1) {  // tape: a draw past the end sets the flag and does not advance
+    const long long avail = X.rng.tape_hi - X.rng.tape_lo - (long long)base;
+    if (nbear > avail) X.rng.err |= 4u;
+    X.rng.ctr += (unsigned long long)(nbear < avail ? nbear : (avail > 0 ? avail : 0));
+  } else {
+    X.rng.ctr += (unsigned long long)nbear;
+  }
+  uint16_t *tl = S.tl + (size_t)me * P.T * E + env;
+  unsigned long long tq = prof_now(S);
+  int tn = 0;
+  for (int q = 0; q < acc.obs_n; q++) {
+    uint32_t pk = COLW(c.observed, q);
+    tl[(size_t)tn * E] = (uint16_t)(pos_x(pk) | (pos_y(pk) << 8));
+    tn++;
+  }
+  tq = prof_acc(S, 21, tq);
+  if (bearm == 0) { COLW(c.tcnt, me) = (uint32_t)tn; return; }
+  uint32_t colj = 0;  // bits of opponent 0's column
+#pragma unroll
+  for (int i = 0; i < NOWN; i++) colj |= 1u << (i * NOPP);
+  // the bearings to evaluate, opponent-major (bit j*NOWN + i): opponents with at
+  // least two, i.e. a fix. One flat loop over them keeps the lanes of a wave
+  // busy (a per-opponent loop would run each opponent's worst-lane count).
+  uint32_t need = 0;
+#pragma unroll
+  for (int j = 0; j < NOPP; j++) {
+    const uint32_t bj = bearm & (colj << j);
+    if (__builtin_popcount(bj) < 2) continue;
+#pragma unroll
+    for (int i = 0; i < NOWN; i++) need |= ((bj >> (i * NOPP + j)) & 1u) << (j * NOWN + i);
+  }
+  int fxr[NOPP], fyr[NOPP];
+#pragma unroll
+  for (int j = 0; j < NOPP; j++) fxr[j] = fyr[j] = 0;
+  uint32_t fok = 0;  // opponent j has a rounded fix inside the grid
+  int curj = -1, cnt = 0;
+  bool zero = false;
+  double sumx = 0.0, sumy = 0.0, mprev = 0.0, xprev = 0.0, yprev = 0.0;
+  // mean of opponent curj's fixes (np.mean, m = cnt-1 < 8 terms: left-to-right)
+  auto flush = [&]() {
+    if (curj < 0) return;
+    if (zero) { X.rng.err |= LNW_ERRF_ZERODIV; return; }
+    const double mx = sumx / (double)(cnt - 1), my = sumy / (double)(cnt - 1);
+    if (!isfinite(mx) || !isfinite(my)) { X.rng.err |= LNW_ERRF_NAN_ROUND; return; }
+    const double rx = rint(mx), ry = rint(my);
+    if (S.ana.ew_log) {  // combatant.py:146-150: (observer position, rounded fix)
+      const int fx = (int)fmin(fmax(rx, -32768.0), 32767.0), fy = (int)fmin(fmax(ry, -32768.0), 32767.0);
+      ana_record(S.ana.ew_log, S.ana.ew_count, S.ana.ew_cap, (uint32_t)(P.env_base + env),
+                 (uint32_t)X.step | (uint32_t)(me >= P.nb) << 16, COLW(c.pos_cur, me),
+                 (uint32_t)(uint16_t)fx | (uint32_t)(uint16_t)fy << 16);
+    }
+    if (!(rx >= 0.0 && rx < (double)P.G && ry >= 0.0 && ry < (double)P.G)) return;
+#pragma unroll
+    for (int j = 0; j < NOPP; j++) {
+      fxr[j] = curj == j ? (int)rx : fxr[j];
+      fyr[j] = curj == j ? (int)ry : fyr[j];
+    }
+    fok |= 1u << curj;
+  };
+  while (need) {
+    const int t = __builtin_ctz(need);
+    need &= need - 1;
+    const int j = t / NOWN, i = t - j * NOWN, b = i * NOPP + j;
+    const uint32_t pi = COLW(c.pos_cur, own0 + i), pj = COLW(c.pos_cur, opp0 + j);
+    const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
+    // math.degrees(math.atan2(dy, dx)): host-libm table in the LOS window
+    const bool tab = S.atan_deg && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS;
+    const double a0 = tab ? S.atan_deg[(dy + R_LOS) * LOS_W + (dx + R_LOS)]
+                          : atan2((double)dy, (double)dx) * RAD2DEG;
+    if (j != curj) {
+      flush();
+      curj = j; cnt = 0; zero = false; sumx = sumy = 0.0;
+    }
+    const int k = __builtin_popcount(bearm & ((1u << b) - 1u));
+    const double g = X.rng.gauss_at(base + (unsigned long long)k);
+    const double bearing = a0 + g < 0 ? a0 + g + 360.0 : a0 + g;  // calculate_bearing (combatant.py:249-263)
+    const double m = tan(bearing * DEG2RAD);
+    const double x1 = pos_x(pi), y1 = pos_y(pi);
+    if (cnt > 0 && !zero) {
+      if (mprev - m == 0.0) {
+        zero = true;
+      } else {
+        double x3, y3;
+        fix_pair(mprev, m, xprev, yprev, x1, y1, x3, y3);
+        sumx += x3;
+        sumy += y3;
+      }
+    }
+    cnt++;
+    mprev = m; xprev = x1; yprev = y1;
+  }
+  flush();
+  tq = prof_acc(S, 22, tq);
+  // fix targets (combatant.py:156-161), opponents in order of their first bearing
+  uint32_t rem = bearm, done = 0;
+  while (rem) {
+    const int b = __builtin_ctz(rem);
+    rem &= rem - 1;
+    const int jj = b % NOPP;
+    if ((done >> jj) & 1u) continue;
+    done |= 1u << jj;
+    if (!((fok >> jj) & 1u)) continue;
+    const int fxi = rsel(fxr, jj), fyi = rsel(fyr, jj);
+#pragma unroll
+    for (int j = 0; j < NOPP; j++) {
+      if (!COLB(c.alive0, opp0 + j)) continue;
+      const uint32_t pj = COLW(c.pos_cur, opp0 + j);
+      const int ddx = pos_x(pj) - fxi, ddy = pos_y(pj) - fyi;
+      if (ddx * ddx + ddy * ddy < 4) {
+        tl[(size_t)tn * E] = (uint16_t)(fxi | (fyi << 8));
+        tn++;
+      }
+    }
+  }
+  COLW(c.tcnt, me) = (uint32_t)tn;
+  prof_acc(S, 23, tq);
+}
+
 // Compile-time ship counts: positions and alive flags of both sides are read
 // into registers once, the 16 (4v4) distance tests run branch-free, and only
-// pairs inside a sensor range take the pair_detect path.
+// pairs inside a sensor range are walked. The walk (pass 1) is integer work: the
+// observed list and which pairs yield an EW bearing; the floating-point part —
+// bearings, gauss draws, tangents and fixes — runs afterwards (finish_obs_t),
+// only for opponents with the two bearings a fix needs. (Keeping the walk's
+// operands in registers instead of LDS measured slower: the kernel is at 256
+// VGPRs and the extra arrays spill to scratch.)
 template <int NOWN, int NOPP>
 __device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
   Cols &c = X.c;
@@ -602,7 +786,6 @@ __device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
     uint32_t p = COLW(c.pos_cur, opp0 + j);
     xp[j] = pos_x(p); yp[j] = pos_y(p);
     amask |= (COLB(c.alive0, opp0 + j) ? 1u : 0u) << (NOWN + j);
-    COLB(c.bcnt, j) = 0;
   }
   uint32_t near = 0;  // bit i*NOPP+j: both alive and within the max sensor range
 #pragma unroll
@@ -614,6 +797,9 @@ __device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
       near |= (in ? 1u : 0u) << (i * NOPP + j);
     }
   ObsAcc acc{0, 0};
+  const unsigned long long tw = prof_now(X.S);
+  const uint64_t lbits = X.lpre[own0 != 0];
+  uint32_t bearm = 0;  // bit i*NOPP+j: pair (i, j) yields a bearing (one gauss draw)
   while (near) {  // pairs in index order (i outer, j inner), as the reference loops
     int b = __builtin_ctz(near);
     near &= near - 1;
@@ -621,10 +807,120 @@ __device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
     uint32_t pi = COLW(c.pos_cur, own0 + i), pj = COLW(c.pos_cur, opp0 + j);
     int xi = pos_x(pi), yi = pos_y(pi), xj = pos_x(pj), yj = pos_y(pj);
     int dx = xj - xi, dy = yj - yi;
-    pair_detect(X, myradar, own0 + i, j, xi, yi, COLB(c.type, own0 + i), xj, yj,
-                COLB(c.type, opp0 + j), COLW(c.radar_cur, opp0 + j), dx * dx + dy * dy, acc);
+    const int d2 = dx * dx + dy * dy;
+    const int ti = COLB(c.type, own0 + i), tj = COLB(c.type, opp0 + j);
+    const int rr = radar_r(X.P, X.duct(), ti, tj), re = ew_r(X.P, X.duct(), ti, tj);
+    const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
+    const bool ew_cand = d2 < re * re && COLW(c.radar_cur, opp0 + j) == 1;
+    if (!(rad_ok || close || ew_cand)) continue;  // LOS result would be unused
+    uint32_t los;
+    if (X.pre) {
+      // own ship i stands on its new cell once its turn has come and it moved
+      const int v = (own0 + i <= me) && (COLW(c.pos_new, own0 + i) & 0x80000000u) ? 1 : 0;
+      los = (uint32_t)(lbits >> (((i * NOPP + j) * 2 + v) * 2)) & 3u;
+    } else {
+      los = los_q(X.P, X.S, X.mask, xi, yi, xj, yj);
+    }
+    if (pair_observe(X, xj, yj, rad_ok, close, ew_cand, los, acc)) bearm |= 1u << b;
   }
-  finish_obs<NOWN, true>(X, me, opp0, opp0 + NOPP, acc);
+  prof_acc(X.S, 20, tw);
+  finish_obs_t<NOWN, NOPP>(X, me, own0, opp0, acc, bearm);
+}
+
+// Every LOS query get_obs can make during this step's agent loop, loaded in one
+// batch before it (the loop otherwise waits on one table load per pair). While
+// blue plays, red ships stand on their old cells and blue ship i on its new cell
+// once its turn has come (i <= me) and it moved; while red plays, blue ships stand
+// on their final cells. So blue->red rays need blue old/new x red
+// old, and red->blue rays red old/new x blue final: 2 * NB * NR * 2 rays at most,
+// fewer when pairs are out of every sensor range or a ship kept its cell.
+template <int NB, int NR>
+__device__ inline void los_prefetch_t(Ctx &X) {
+  const KParams &P = X.P;
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  constexpr int NPAIR = NB * NR;
+  static_assert(NPAIR * 4 <= 64, "LOS prefetch bits exceed 64 per side");
+  int bo[NB], bn[NB], ro[NR], rn[NR];  // packed x<<8|y cells: old, final
+  uint32_t bmv = 0, rmv = 0, al = 0;
+#pragma unroll
+  for (int i = 0; i < NB; i++) {
+    const uint32_t po = COLW(c.pos_cur, i), pn = COLW(c.pos_new, i);
+    const bool mv = (pn & 0x80000000u) != 0;
+    bo[i] = pos_x(po) << 8 | pos_y(po);
+    bn[i] = mv ? (pos_x(pn & 0x7fffffffu) << 8 | pos_y(pn & 0x7fffffffu)) : bo[i];
+    bmv |= (mv ? 1u : 0u) << i;
+    al |= (COLB(c.alive0, i) ? 1u : 0u) << i;
+  }
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const uint32_t po = COLW(c.pos_cur, NB + j), pn = COLW(c.pos_new, NB + j);
+    const bool mv = (pn & 0x80000000u) != 0;
+    ro[j] = pos_x(po) << 8 | pos_y(po);
+    rn[j] = mv ? (pos_x(pn & 0x7fffffffu) << 8 | pos_y(pn & 0x7fffffffu)) : ro[j];
+    rmv |= (mv ? 1u : 0u) << j;
+    al |= (COLB(c.alive0, NB + j) ? 1u : 0u) << (NB + j);
+  }
+  // ray r: side s = r / (2*NPAIR); within a side, ((own*NOPP + opp)*2 + v)
+  auto ray = [&](int r, int &x1, int &y1, int &x2, int &y2, bool &need) {
+    const int s = r / (2 * NPAIR), q = r % (2 * NPAIR), v = q & 1, p = q >> 1;
+    int o, d;
+    if (s == 0) {
+      const int i = p / NR, j = p % NR;
+      o = v ? bn[i] : bo[i];
+      d = ro[j];
+      need = ((al >> i) & (al >> (NB + j)) & 1u) && (v == 0 || ((bmv >> i) & 1u));
+    } else {
+      const int j = p / NB, i = p % NB;
+      o = v ? rn[j] : ro[j];
+      d = bn[i];
+      need = ((al >> i) & (al >> (NB + j)) & 1u) && (v == 0 || ((rmv >> j) & 1u));
+    }
+    x1 = o >> 8; y1 = o & 255; x2 = d >> 8; y2 = d & 255;
+    const int dx = x2 - x1, dy = y2 - y1;
+    need = need && dx * dx + dy * dy < X.r2max;
+  };
+  uint64_t bits[2] = {0, 0};
+  constexpr int NRAY = 4 * NPAIR;
+  constexpr int CH = 16;
+#pragma unroll
+  for (int r0 = 0; r0 < NRAY; r0 += CH) {
+    uint32_t wi[CH], tabm = 0, marchm = 0;
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      wi[u] = 0;
+      if (r0 + u >= NRAY) continue;
+      int x1, y1, x2, y2;
+      bool need;
+      ray(r0 + u, x1, y1, x2, y2, need);
+      const int dx = x2 - x1, dy = y2 - y1;
+      const bool tab = dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS;
+      tabm |= (need && tab ? 1u : 0u) << u;
+      marchm |= (need && !tab ? 1u : 0u) << u;
+      wi[u] = ((uint32_t)(x1 * P.G + y1) * LOS_CELL_WORDS + (dx + R_LOS) * LOS_ROW_WORDS) * 32u +
+              (dy + R_LOS) * 2;
+    }
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      if (r0 + u >= NRAY) continue;
+      const uint32_t w = (tabm >> u) & 1u ? S.lostab[wi[u] >> 5] : 0u;
+      const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR);
+      bits[s] |= (uint64_t)((w >> (wi[u] & 31)) & 3u) << (2 * q);
+    }
+    while (marchm) {  // outside the table window (very long sensor ranges)
+      const int u = __builtin_ctz(marchm);
+      marchm &= marchm - 1;
+      int x1, y1, x2, y2;
+      bool need;
+      ray(r0 + u, x1, y1, x2, y2, need);
+      const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR);
+      bits[s] |= (uint64_t)los_march<true>(X.mask, P.W16, x1, y1, x2, y2) << (2 * q);
+    }
+  }
+  X.lpre[0] = bits[0];
+  X.lpre[1] = bits[1];
+  X.pre = true;
 }
 
 // check_target (combatant.py:570-584): first live opponent within 3.5 cells
@@ -1484,12 +1780,15 @@ __device__ __forceinline__ bool move_phase(const KParams &P, const KState &S, Co
 }
 
 // diagnostics: per-workgroup phase timestamps (100 MHz real-time clock)
+// slots: 0 start, 4 L end, 1 S start, 3 wave-0 end, 5 wave-1 end, 6..13 agent
+// ends (phase S) or 6..9 quiet-path marks, 14 quiet marker, 16..19 lane-0 phase-S
+// section totals (take_action to the move, LOS prefetch, get_obs, reward), 20..23 get_obs parts
 __device__ inline void prof_put(const KState &S, int slot, unsigned long long v) {
-  if (S.prof && (threadIdx.x & (WAVE - 1)) == 0) S.prof[(size_t)blockIdx.x * 16 + slot] = v;
+  if (S.prof && (threadIdx.x & (WAVE - 1)) == 0) S.prof[(size_t)blockIdx.x * PROF_SLOTS + slot] = v;
 }
 __device__ inline void prof_stamp(const KState &S, int slot) {
   if (S.prof && (threadIdx.x & (WAVE - 1)) == 0)
-    S.prof[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+    S.prof[(size_t)blockIdx.x * PROF_SLOTS + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Game.step tail (game.py:409-520) for the env in LDS column `lane` once every
@@ -1710,6 +2009,11 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     if (emit) publish_progress(&prog, 0);
     Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), emit ? S.mask2 : mask, E,
           r2col[lane], 0};
+    unsigned long long tp[4] = {0, 0, 0, 0}, t0 = prof_now(S);  // LNW_PROF part totals
+    if constexpr (ST) {
+      if (P.los_mode == 0 && !(P.dbg_skip & 2048)) los_prefetch_t<NB, NR>(X);
+    }
+    tp[1] += prof_now(S) - t0;
     Neut N{{0, 0}, {0u, 0u}};
     int ev[8];
 #pragma unroll
@@ -1718,79 +2022,94 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     int hits[2] = {0, 0};
     int bsx = 0, bsy = 0, rsx = 0, rsy = 0;  // exact integer sums
     int nbp = 0, nrp = 0;
+    // each agent in three sections that reconverge (take_action up to the move,
+    // get_obs, reward), so the LNW_PROF section timers measure the wave
     for (int a = 0; a < A; a++) {
-     do {
-      if (!COLB(c.alive0, a)) { COLW(c.reward, a) = 0.0; break; }
+      const bool al = COLB(c.alive0, a) != 0;  // sunk ships skip their turn (reward 0)
       const int side = a >= nb;
-      uint32_t p0 = COLW(c.pos_cur, a);
-      if (!side) {
-        if (P.side_blue) { bsx += pos_x(p0); bsy += pos_y(p0); nbp++; }
-      } else {
-        rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
-      }
-      size_t row = ((size_t)env * A + a) * 4;
-      double a0 = COLW(c.act0, a), a1 = COLW(c.act1, a);
-      int kind = COLB(c.akind, a);
-      // untrained red: random salvo (game.py:375-379), written back in place
-      if (side && !P.trained_red) {
-        if (X.rng.uniform() < P.red_aggression) {
-          double v = X.rng.uniform();
-          if (dt == LNW_ACT_F32) { float f = (float)v; ((float *)actions)[row + 1] = f; a1 = f; }
-          else if (dt == LNW_ACT_F64) {
-            if (kind == K_F32) v = (double)(float)v;
-            ((double *)actions)[row + 1] = v; a1 = v;
-          } else { ((int32_t *)actions)[row + 1] = 0; a1 = 0.0; }
-        }
-      }
-      // take_action (combatant.py:501-565)
-      double engagement = P.discrete ? rint(a1) : a1;
-      int keng = P.discrete ? K_PYINT : kind;
-      int mk = COLB(c.mkind, a);
-      double thr_v;
-      if (kind_promote(keng, mk) == K_F32)
-        thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
-      else
-        thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
-      bool engage = thr_v > 0.0;
+      bool engage = false, moved = false;
       int destroyed = 0;
-      int tn = (int)COLW(c.tcnt, a);
-      if (engage && tn > 0) {
-        const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
-        for (int q = 0; q < tn; q++) {
-          uint16_t tg = tl[(size_t)q * E];
-          if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+      t0 = prof_now(S);
+      if (al) {
+        uint32_t p0 = COLW(c.pos_cur, a);
+        if (!side) {
+          if (P.side_blue) { bsx += pos_x(p0); bsy += pos_y(p0); nbp++; }
+        } else {
+          rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
+        }
+        size_t row = ((size_t)env * A + a) * 4;
+        double a0 = COLW(c.act0, a), a1 = COLW(c.act1, a);
+        int kind = COLB(c.akind, a);
+        // untrained red: random salvo (game.py:375-379), written back in place
+        if (side && !P.trained_red) {
+          if (X.rng.uniform() < P.red_aggression) {
+            double v = X.rng.uniform();
+            if (dt == LNW_ACT_F32) { float f = (float)v; ((float *)actions)[row + 1] = f; a1 = f; }
+            else if (dt == LNW_ACT_F64) {
+              if (kind == K_F32) v = (double)(float)v;
+              ((double *)actions)[row + 1] = v; a1 = v;
+            } else { ((int32_t *)actions)[row + 1] = 0; a1 = 0.0; }
+          }
+        }
+        // take_action (combatant.py:501-565)
+        double engagement = P.discrete ? rint(a1) : a1;
+        int keng = P.discrete ? K_PYINT : kind;
+        int mk = COLB(c.mkind, a);
+        double thr_v;
+        if (kind_promote(keng, mk) == K_F32)
+          thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
+        else
+          thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
+        engage = thr_v > 0.0;
+        int tn = (int)COLW(c.tcnt, a);
+        if (engage && tn > 0) {
+          const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
+          for (int q = 0; q < tn; q++) {
+            uint16_t tg = tl[(size_t)q * E];
+            if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+          }
+        }
+        if (side) ev[6] += destroyed; else ev[5] += destroyed;
+        if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
+        else {
+          double rr = rint(a0);
+          COLW(c.radar_cur, a) = (int)fmin(fmax(rr, -2147483648.0), 2147483647.0);
+        }
+        uint32_t pn = COLW(c.pos_new, a);
+        moved = (pn & 0x80000000u) != 0;
+        if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
+      }
+      tp[0] += prof_now(S) - t0;
+      t0 = prof_now(S);
+      if (al && !(P.dbg_skip & 128)) {
+        if constexpr (ST) {
+          if (!side) get_obs_t<NB, NR>(X, a, 0, NB);
+          else get_obs_t<NR, NB>(X, a, NB, 0);
+        } else {
+          get_obs_dev(X, a);
         }
       }
-      if (side) ev[6] += destroyed; else ev[5] += destroyed;
-      if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
-      else {
-        double rr = rint(a0);
-        COLW(c.radar_cur, a) = (int)fmin(fmax(rr, -2147483648.0), 2147483647.0);
-      }
-      uint32_t pn = COLW(c.pos_new, a);
-      bool moved = (pn & 0x80000000u) != 0;
-      if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
-      if (P.dbg_skip & 128) {
-      } else if constexpr (ST) {
-        if (!side) get_obs_t<NB, NR>(X, a, 0, NB);
-        else get_obs_t<NR, NB>(X, a, NB, 0);
-      } else {
-        get_obs_dev(X, a);
-      }
-      double r = (P.dbg_skip & 256) ? 0.0 : reward_dev(X, a, moved, engage, destroyed);
+      tp[2] += prof_now(S) - t0;
+      t0 = prof_now(S);
+      double r = 0.0;
+      if (al && !(P.dbg_skip & 256)) r = reward_dev(X, a, moved, engage, destroyed);
       COLW(c.reward, a) = r;
-      if (!side) {
-        if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
-      } else {
-        if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
+      if (al) {
+        if (!side) {
+          if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
+        } else {
+          if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
+        }
+        hits[side] += destroyed;
       }
-      hits[side] += destroyed;
-     } while (0);
+      tp[3] += prof_now(S) - t0;
       if (emit) publish_progress(&prog, a + 1);
       if (a < 8) prof_stamp(S, 6 + a);
     }
     env_tail(P, S, c, lane, env, nb, A, N, ev, hits, nbp, nrp, bsx, bsy, rsx, rsy, X.rng, rew_b,
              rew_r, done_out, cog_out);
+    if (S.prof && lane == 0)
+      for (int q = 0; q < 4; q++) prof_put(S, 16 + q, tp[q]);
   }
   prof_stamp(S, 3);
   if ((P.dbg_skip & 1) || emit) return;
@@ -2070,7 +2389,7 @@ struct lnw_handle {
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
   uint8_t *miss = nullptr, *mkind = nullptr, *alive = nullptr, *type = nullptr;
-  double *dist_lz = nullptr, *duct = nullptr, *bear_val = nullptr;
+  double *dist_lz = nullptr, *duct = nullptr, *bear_val = nullptr, *d_atan = nullptr;
   uint8_t *bear_ship = nullptr;
   uint16_t *tl_cnt = nullptr, *tl = nullptr;
   unsigned long long *rng = nullptr;
@@ -2099,7 +2418,7 @@ KState make_state(lnw_handle *h) {
   s.pos = h->pos; s.radar = h->radar; s.miss = h->miss; s.mkind = h->mkind; s.alive = h->alive;
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
-  s.bear_val = h->bear_val; s.bear_ship = h->bear_ship;
+  s.bear_val = h->bear_val; s.bear_ship = h->bear_ship; s.atan_deg = h->d_atan;
   s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.ana = h->ana; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
@@ -2146,22 +2465,24 @@ int choose_epw(const lnw_handle *h) {
 // LNW_PROF diagnostics: mean per-workgroup phase spans and the grid-wide
 // start / end spread of one step launch (synchronises the stream).
 void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
-  std::vector<unsigned long long> t((size_t)nwg * 16);
+  std::vector<unsigned long long> t((size_t)nwg * PROF_SLOTS);
   if (hipMemcpyAsync(t.data(), h->d_prof, t.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return;
-  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0, sa[8] = {0}, sq[4] = {0};
+  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0, sa[8] = {0}, sq[4] = {0}, sp[4] = {0}, sg[4] = {0};
   int nq = 0;
   unsigned long long t0 = ~0ull, tend0 = 0, tend1 = 0;
   int n1 = 0;
   for (int w = 0; w < nwg; w++) {
-    const unsigned long long *r = &t[(size_t)w * 16];
+    const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
     sL += (double)(r[4] - r[0]);
     sM += (double)(r[1] - r[4]);
     sS += (double)(r[2] - r[1]);
     sW += (double)(r[3] - r[2]);
     if (r[5]) { s1 += (double)(r[5] - r[0]); n1++; if (r[5] > tend1) tend1 = r[5]; }
-    if (r[9]) {  // quiet workgroup: M end | A* + barrier | predicate | phase Q + barrier
+    for (int q = 0; q < 4; q++) sp[q] += (double)r[16 + q];
+    for (int q = 0; q < 4; q++) sg[q] += (double)r[20 + q];
+    if (r[14]) {  // quiet workgroup: M end | A* + barrier | predicate | phase Q + barrier
       nq++;
       sq[0] += (double)(r[6] - r[4]);
       sq[1] += (double)(r[7] - r[6]);
@@ -2182,9 +2503,15 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
   if (nq)
     fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us\n",
             nq, sq[0] / nq * us, sq[1] / nq * us, sq[2] / nq * us, sq[3] / nq * us);
-  fprintf(stderr, "[lnw prof] phase S per agent (us):");
-  for (int a = 0; a < 8; a++) fprintf(stderr, " %.2f", sa[a] / nwg * us);
-  fprintf(stderr, "\n");
+  const int ns = nwg - nq;
+  fprintf(stderr, "[lnw prof] phase S workgroups %d, per agent (us):", ns);
+  for (int a = 0; a < 8; a++) fprintf(stderr, " %.2f", ns ? sa[a] / ns * us : 0.0);
+  fprintf(stderr, "; section totals take_action %.2f, LOS prefetch %.2f, get_obs %.2f, reward %.2f us\n",
+          ns ? sp[0] / ns * us : 0.0, ns ? sp[1] / ns * us : 0.0, ns ? sp[2] / ns * us : 0.0,
+          ns ? sp[3] / ns * us : 0.0);
+  fprintf(stderr, "[lnw prof] get_obs parts (templated): pair walk %.2f, observed stores %.2f, bearings+fixes %.2f, fix targets %.2f us\n",
+          ns ? sg[0] / ns * us : 0.0, ns ? sg[1] / ns * us : 0.0, ns ? sg[2] / ns * us : 0.0,
+          ns ? sg[3] / ns * us : 0.0);
 }
 
 extern "C" {
@@ -2251,10 +2578,20 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   rc |= dalloc(h, &h->sp_pos, 128);
   rc |= dalloc(h, &h->sp_randls, 64);
   rc |= dalloc(h, &h->d_dummy, 4 * 64);
+  rc |= dalloc(h, &h->d_atan, (size_t)LOS_W * LOS_W);
   if (rc) {
     std::string m = g_err;
     lnw_destroy(h);
     return fail(LNW_ENOMEM, m);
+  }
+  {  // EW bearing table: math.degrees(math.atan2(dy, dx)) for integer offsets in
+     // [-R_LOS, R_LOS]^2, computed by the host libm as the reference does
+     // (combatant.py:253), so the device needs no atan2 of its own in range
+    std::vector<double> at((size_t)LOS_W * LOS_W);
+    for (int dy = -R_LOS; dy <= R_LOS; dy++)
+      for (int dx = -R_LOS; dx <= R_LOS; dx++)
+        at[(size_t)(dy + R_LOS) * LOS_W + (dx + R_LOS)] = atan2((double)dy, (double)dx) * (180.0 / PY_PI);
+    HIPCHK(hipMemcpy(h->d_atan, at.data(), at.size() * sizeof(double), hipMemcpyHostToDevice));
   }
   KParams &k = h->kp;
   k.discrete = params->discrete; k.landing_ops = params->landing_ops;
@@ -2420,8 +2757,8 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
   if (h->prof) {
-    if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * 16 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(h->d_prof, 0, (size_t)grid.x * 16 * sizeof(unsigned long long), st));
+    if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * PROF_SLOTS * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(h->d_prof, 0, (size_t)grid.x * PROF_SLOTS * sizeof(unsigned long long), st));
     s.prof = h->d_prof;
   }
   bool generic = h->force_generic;
