@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tgpu.log 2>&1 || { tail -30 gpurun_out/tgpu.log; exit 1; }
+tail -1 gpurun_out/tgpu.log
+for i in 1 2; do
+timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 3
+python -c "import json; d=json.load(open('gpurun_out/bench.json')); print('REF', d['value']/1e6, 'M', d['roofline']['kernel_ms_mean']*1e3, 'us')"
+done
+LNW_PROF=1 timeout -k 10 300 python bench.py --steps 3 --warmup 5 --no-cpu-baseline > gpurun_out/pr.json 2> gpurun_out/pr.err || exit 5
+grep "lnw prof" gpurun_out/pr.err | tail -4 | head -2
