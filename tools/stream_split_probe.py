@@ -43,6 +43,9 @@ def main():
                 with torch.cuda.stream(streams[s]):
                     g = BatchedGame(Es, ["small"] * 4, ["large"] * 4, scenario=sc,
                                     device=torch.cuda.current_device(), env_id_base=s * Es, seed=1234)
+                    # 64 envs per workgroup (full waves: the quiet path) so each
+                    # shard's grid takes only its share of the resident slots
+                    assert L.lnw_set_epw(g.h, 64) == 64
                     g.reset(positions=bench.REF_BLUE + bench.REF_RED)
                     a = torch.empty((NA, Es, 8, 4), dtype=torch.float32, device="cuda")
                     for k in range(NA):
