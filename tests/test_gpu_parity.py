@@ -541,3 +541,49 @@ def test_quiet_path_vs_phase_s_long(grids, spawns):
         assert np.array_equal(a, b, equal_nan=True), f
     for g in games:
         g.close()
+
+
+@pytest.mark.parametrize("duct", [2.9, 4.5])
+def test_philox_long_sensor_ranges_vs_oracle(grids, duct):
+    """Ducting far above the reference's 1+Beta(1,3) < 2 (set through the state
+    API) stretches EW ranges past the 40-cell LOS-table / bearing-table window:
+    the batched LOS prefetch falls back to the ray march and the deferred
+    bearings to the device atan2 for those pairs. 64 envs (one full two-wave
+    workgroup), sides 20-50 cells apart, Philox mode, bit-exact against the CPU
+    oracle with the same ducting."""
+    import _oracle
+    from lnw._abi import F_DUCT
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    grid = grids[0]
+    E, S = 64, 8
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+                    grid=grid, seed=5)
+    assert g.set_epw(64) == 64
+    pos = _melee_positions(grid, E, 4, 4, seed=int(duct * 10), box_b=(20, 35, 35, 65),
+                           box_r=(60, 75, 35, 65))
+    g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
+    g.set(F_DUCT, torch.full((E,), duct, dtype=torch.float64))
+    oracles = []
+    for e in range(E):
+        o = _oracle.OracleEnv(grid, 4, 4)
+        o.set_philox(5, e)
+        o.reset([0] * 4 + [1] * 4, pos[e])
+        o.set_ducting(duct)
+        oracles.append(o)
+    rng = np.random.default_rng(int(duct * 100))
+    for s in range(S):
+        act = rng.random((E, 8, 4)).astype(np.float32)
+        out = g.step(torch.from_numpy(act).cuda())
+        ob, orr = out["obs_blue"].cpu().numpy(), out["obs_red"].cpu().numpy()
+        rb, rr = out["rew_blue"].cpu().numpy(), out["rew_red"].cpu().numpy()
+        for e in range(E):
+            r = oracles[e].step(act[e], np.full(8, _oracle.K_F32, np.int32))
+            assert np.array_equal(ob[e], r["obs_blue"].astype(np.float32)), (s, e, "obs_blue")
+            assert np.array_equal(orr[e], r["obs_red"].astype(np.float32)), (s, e, "obs_red")
+            assert np.allclose(rb[e], r["rew_blue"], rtol=0, atol=REW_TOL), (s, e, "rew_blue")
+            assert np.allclose(rr[e], r["rew_red"], rtol=0, atol=REW_TOL), (s, e, "rew_red")
+    st = g.env_state()
+    for e in range(E):
+        assert st["err"][e] == oracles[e].env_state()["err"], e
+    g.close()
