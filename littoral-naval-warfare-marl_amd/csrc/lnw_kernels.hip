@@ -1972,7 +1972,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   const bool astar = NW > 1 ? __syncthreads_or(pend) != 0 : true;
   // quiet workgroups (lnw_quiet.inc) skip phase S; deciding it needs the final
   // moves, so wave 0 runs the A* fallback before a second barrier
-  const bool qcap = emit && P.trained_red && !(P.dbg_skip & 512);
+  const bool qcap = emit && !(P.dbg_skip & 512);
   if constexpr (ST && NW > 1) {
     if (qcap) {
       if (wid == 0) prof_stamp(S, 6);
@@ -1984,8 +1984,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       const bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
       if (wid == 0) prof_stamp(S, 8);
       if (wq) {
-        quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, obs_b, obs_r, rew_b, rew_r,
-                             done_out, cog_out, env0);
+        quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
+                             rew_r, done_out, cog_out, env0);
         return;
       }
     }

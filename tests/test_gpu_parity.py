@@ -465,17 +465,21 @@ def test_config4_launch_shape_invariance(grids):
 REF_SPAWNS = [(6, 61), (10, 81), (8, 70), (11, 58), (98, 48), (98, 52), (98, 56), (96, 52)]
 
 
-def test_quiet_path_vs_oracle(grids):
+@pytest.mark.parametrize("trained_red", [True, False])
+def test_quiet_path_vs_oracle(grids, trained_red):
     """Quiet workgroups (lnw_quiet.inc): 128 envs at 64 per workgroup in Philox
     mode; workgroup 0 holds reference spawns (quiet: no sensor contact, phase Q
     + whole-block emission), workgroup 1 half reference, half split spawns (not
-    quiet: phase S). Every output bit-exact against the CPU oracle."""
+    quiet: phase S). Every output bit-exact against the CPU oracle; with an
+    untrained red also its random salvos (game.py:375-379: the draws and the
+    in-place action writes)."""
     import _oracle
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
     grid = grids[0]
     E, S = 128, 14
-    g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4,
+                    scenario=Scenario(landing_ops=False, trained_red=trained_red),
                     grid=grid, seed=21)
     assert g.set_epw(64) == 64
     pos = np.array([REF_SPAWNS] * E, np.int32)
@@ -483,19 +487,22 @@ def test_quiet_path_vs_oracle(grids):
     g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
     oracles = []
     for e in range(E):
-        o = _oracle.OracleEnv(grid, 4, 4)
+        o = _oracle.OracleEnv(grid, 4, 4, trained_red=trained_red)
         o.set_philox(21, e)
         o.reset([0] * 4 + [1] * 4, pos[e])
         oracles.append(o)
     rng = np.random.default_rng(8)
     for s in range(S):
         act = rng.random((E, 8, 4)).astype(np.float32)
-        out = g.step(torch.from_numpy(act).cuda())
+        act_dev = torch.from_numpy(act).cuda()
+        out = g.step(act_dev)
+        act_after = act_dev.cpu().numpy()
         ob, orr = out["obs_blue"].cpu().numpy(), out["obs_red"].cpu().numpy()
         rb, rr = out["rew_blue"].cpu().numpy(), out["rew_red"].cpu().numpy()
         dn, cg = out["done"].cpu().numpy(), out["cog"].cpu().numpy()
         for e in range(E):
             r = oracles[e].step(act[e], np.full(8, _oracle.K_F32, np.int32))
+            assert np.array_equal(act_after[e], r["actions_after"].astype(np.float32)), (s, e, "actions")
             assert np.array_equal(ob[e], r["obs_blue"].astype(np.float32)), (s, e, "obs_blue")
             assert np.array_equal(orr[e], r["obs_red"].astype(np.float32)), (s, e, "obs_red")
             assert np.allclose(rb[e], r["rew_blue"], rtol=0, atol=REW_TOL), (s, e, "rew_blue")
@@ -505,8 +512,9 @@ def test_quiet_path_vs_oracle(grids):
     g.close()
 
 
+@pytest.mark.parametrize("trained_red", [True, False])
 @pytest.mark.parametrize("spawns", ["reference", "mixed"])
-def test_quiet_path_vs_phase_s_long(grids, spawns):
+def test_quiet_path_vs_phase_s_long(grids, spawns, trained_red):
     """The bench workload shape (auto-reset, 40-step episodes, Philox) over 90
     steps: 64 envs per workgroup (quiet path where it applies) against 16 per
     workgroup (phase S + phase O everywhere): identical observations, rewards,
@@ -515,7 +523,7 @@ def test_quiet_path_vs_phase_s_long(grids, spawns):
     from lnw import _abi
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
-    sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40)
+    sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40, trained_red=trained_red)
     E = 256
     pos = np.array([REF_SPAWNS] * E, np.int32)
     if spawns == "mixed":
@@ -530,9 +538,11 @@ def test_quiet_path_vs_phase_s_long(grids, spawns):
     rng = np.random.default_rng(2)
     for s in range(90):
         act = torch.from_numpy(rng.random((E, 8, 4)).astype(np.float32)).cuda()
-        outs = [{k: v.cpu().numpy().copy() for k, v in g.step(act.clone()).items()} for g in games]
+        acts = [act.clone() for _ in games]
+        outs = [{k: v.cpu().numpy().copy() for k, v in g.step(a).items()} for g, a in zip(games, acts)]
         for k in outs[0]:
             assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), (s, k)
+        assert torch.equal(acts[0], acts[1]), (s, "actions written back")
     sts = [g.env_state() for g in games]
     for k in sts[0]:
         assert np.array_equal(sts[0][k], sts[1][k], equal_nan=True), k
