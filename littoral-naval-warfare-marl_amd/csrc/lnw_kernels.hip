@@ -335,9 +335,18 @@ __device__ inline bool pair_observe(Ctx &X, int xj, int yj, bool rad_ok, bool cl
   return ew_cand && (los & 2u) && !seen;
 }
 
+// math.degrees(math.atan2(dy, dx)) (combatant.py:253): the host-libm table in
+// the +-R_LOS window, the device atan2 outside it (or with LNW_DEBUG_SKIP bit 12)
+__device__ inline double bearing_deg(const KParams &P, const KState &S, int dx, int dy) {
+  const bool tab = !(P.dbg_skip & 4096) && S.atan_deg && dx >= -R_LOS && dx <= R_LOS &&
+                   dy >= -R_LOS && dy <= R_LOS;
+  return tab ? S.atan_deg[(dy + R_LOS) * LOS_W + (dx + R_LOS)] : atan2((double)dy, (double)dx) * RAD2DEG;
+}
+
 // calculate_bearing (combatant.py:249-263) with the gauss draw given
-__device__ inline double ew_bearing(int xi, int yi, int xj, int yj, double distortion) {
-  double bearing = atan2((double)(yj - yi), (double)(xj - xi)) * RAD2DEG;
+__device__ inline double ew_bearing(const KParams &P, const KState &S, int xi, int yi, int xj, int yj,
+                                    double distortion) {
+  double bearing = bearing_deg(P, S, xj - xi, yj - yi);
   if (bearing + distortion < 0)
     bearing = bearing + distortion + 360.0;
   else
@@ -353,7 +362,7 @@ __device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int
   Cols &c = X.c;
   const int lane = X.lane;
   if (pair_observe(X, xj, yj, rad_ok, close, ew_cand, los, acc)) {
-    const double bearing = ew_bearing(xi, yi, xj, yj, X.rng.gauss());
+    const double bearing = ew_bearing(X.P, S, xi, yi, xj, yj, X.rng.gauss());
     int k = COLB(c.bcnt, jj);
     if (k == 0) { COLB(c.border, acc.norder) = (uint8_t)jj; acc.norder++; }
     size_t slot = (size_t)(jj * S.nmax + k) * X.E + X.env;
@@ -706,10 +715,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const Ob
     const int j = t / NOWN, i = t - j * NOWN, b = i * NOPP + j;
     const uint32_t pi = COLW(c.pos_cur, own0 + i), pj = COLW(c.pos_cur, opp0 + j);
     const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
-    // math.degrees(math.atan2(dy, dx)): host-libm table in the LOS window
-    const bool tab = S.atan_deg && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS;
-    const double a0 = tab ? S.atan_deg[(dy + R_LOS) * LOS_W + (dx + R_LOS)]
-                          : atan2((double)dy, (double)dx) * RAD2DEG;
+    const double a0 = bearing_deg(P, S, dx, dy);
     if (j != curj) {
       flush();
       curj = j; cnt = 0; zero = false; sumx = sumy = 0.0;
