@@ -195,9 +195,22 @@ def mappo_rollout(E=32768, T=40, reps=3):
         r.run(generator=gen)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
+    # the same rollout replayed from a HIP graph (Rollout.capture): no host work
+    # between the ~30 kernels of a step
+    g.reset(positions=REF_BLUE + REF_RED)
+    r.capture(generator=gen)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.reset(positions=REF_BLUE + REF_RED)
+        r.replay()
+    torch.cuda.synchronize()
+    dtg = (time.perf_counter() - t0) / reps
     g.close()
-    return dict(env_steps_per_sec=E * T / dt, ms_per_rollout=dt * 1e3, envs=E, steps=T,
-                policy="batched actor (network.py MLP) + critic (Value), fp32")
+    return dict(env_steps_per_sec=E * T / dtg, ms_per_rollout=dtg * 1e3,
+                eager_env_steps_per_sec=E * T / dt, eager_ms_per_rollout=dt * 1e3, envs=E, steps=T,
+                policy="batched actor (network.py MLP) + critic (Value), fp32; HIP-graph replay "
+                       "(eager loop alongside)")
 
 
 def cpu_baseline(seconds, threads):

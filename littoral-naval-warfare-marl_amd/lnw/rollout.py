@@ -122,7 +122,7 @@ class BatchedActor(nn.Module):
         ok = ~(torch.isnan(mean).any(1) | torch.isnan(std).any(1))
         mean_s = torch.where(ok[:, None], mean, torch.zeros_like(mean))
         std_s = torch.where(ok[:, None], std, torch.ones_like(std))
-        dist = Normal(mean_s, std_s)
+        dist = Normal(mean_s, std_s, validate_args=False)  # no host sync (graph capture)
         eps = torch.randn(mean.shape, generator=generator, device=mean.device, dtype=mean.dtype)
         actions = mean_s + std_s * eps
         if noise is not None:
@@ -287,3 +287,30 @@ class Rollout:
         return dict(obs=obs, actions=acts, log_probs=logp, rewards=rew, values=val,
                     running=running, rtg=rtg,
                     gae=gae(rew.mean(2), val, self.gamma) if self.critic is not None else None)
+
+    def capture(self, generator=None):
+        """Record one whole rollout (T steps of actor, red, critic, step kernel and
+        buffer writes, then reward-to-go and GAE) as a HIP graph, so `replay()`
+        launches its ~30 kernels per step without host work in between. One eager
+        rollout runs first on a side stream (lazy initialisation, GEMM heuristics)
+        and advances the envs; reset before replaying. The graph freezes the
+        step launch's parameters (scenario, spawn spec) and the buffers it
+        returns: `replay()` overwrites them in place."""
+        dev = self.g.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            self.run(generator)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        if generator is not None:
+            graph.register_generator_state(generator)
+        with torch.cuda.graph(graph):
+            out = self.run(generator)
+        self._graph, self._graph_out = graph, out
+        return out
+
+    def replay(self):
+        """One rollout from the envs' current state through the captured graph."""
+        self._graph.replay()
+        return self._graph_out

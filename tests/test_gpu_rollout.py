@@ -125,3 +125,30 @@ def test_actor_device_matches_reference():
     np.testing.assert_allclose(mean.cpu().numpy(), gold["tr_mean"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(std.cpu().numpy(), gold["tr_std"], rtol=1e-5, atol=0)
     np.testing.assert_allclose(lp.cpu().numpy(), gold["tr_lp"], rtol=0, atol=1e-4)
+
+
+def test_rollout_graph_replay_matches_eager():
+    """Rollout.capture / replay (HIP graph of a whole rollout) against the eager
+    run from the same env state and generator state: identical buffers."""
+    from lnw import _abi
+    from lnw.rollout import BatchedActor, BatchedCritic, Rollout
+    E, T = 512, 10
+    g = _game(E, seed=5)
+    torch.manual_seed(2)
+    actor = BatchedActor.for_obs(g.Db).cuda()
+    critic = BatchedCritic(g.Db * g.nb).cuda()
+    gen = torch.Generator(device="cuda")
+    r = Rollout(g, actor, critic, steps=T, noise=0.05)
+    r.capture(generator=gen)
+    g.reset(positions=REF_BLUE + REF_RED, box=((40, 40), (57, 65)))
+    snap = {f: g.get(f).clone() for f in range(_abi.F_ERR + 1)}  # incl. RNG counters
+    gen.manual_seed(11)
+    eager = {k: v.clone() for k, v in r.run(generator=gen).items() if v is not None}
+    for f, v in snap.items():
+        g.set(f, v)
+    gen.manual_seed(11)
+    out = r.replay()
+    torch.cuda.synchronize()
+    for k, v in eager.items():
+        assert torch.equal(out[k], v), k
+    g.close()
