@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 runs of gpu_prof.sh into profiles/<tag>_*.
+"""Summarise the rocprofv3 runs of tools/gpu/prof_r01.sh into profiles/<tag>_*.
 
 Reads gpurun_out/prof_kt (kernel trace + stats) and the separate --pmc passes
 (prof_fetch, prof_write, prof_sq, prof_sq2), writes
