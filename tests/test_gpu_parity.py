@@ -597,3 +597,62 @@ def test_philox_long_sensor_ranges_vs_oracle(grids, duct):
     for e in range(E):
         assert st["err"][e] == oracles[e].env_state()["err"], e
     g.close()
+
+
+@pytest.mark.parametrize("trained_red", [True, False])
+@pytest.mark.parametrize("mode", ["f64_mixed_kinds", "i32_discrete"])
+def test_quiet_path_dtypes_vs_oracle(grids, mode, trained_red):
+    """The quiet path with float64 action rows of mixed value kinds (Python
+    float / np.float32 / np.float64 rows, NEP 50) and with DISCRETE int32
+    actions, trained and untrained red: 128 envs at 64 per workgroup (workgroup
+    0 quiet, workgroup 1 half in contact), Philox mode, outputs and the
+    written-back action rows bit-exact against the CPU oracle."""
+    import _oracle
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    grid = grids[0]
+    E, S = 128, 12
+    discrete = mode == "i32_discrete"
+    g = BatchedGame(E, ["small"] * 4, ["large"] * 4,
+                    scenario=Scenario(landing_ops=False, trained_red=trained_red, discrete=discrete),
+                    grid=grid, seed=31)
+    assert g.set_epw(64) == 64
+    pos = np.array([REF_SPAWNS] * E, np.int32)
+    pos[96:] = _melee_positions(grid, 32, 4, 4, seed=6)
+    g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
+    oracles = []
+    for e in range(E):
+        o = _oracle.OracleEnv(grid, 4, 4, trained_red=trained_red, discrete=discrete)
+        o.set_philox(31, e)
+        o.reset([0] * 4 + [1] * 4, pos[e])
+        oracles.append(o)
+    rng = np.random.default_rng(17 + int(trained_red))
+    for s in range(S):
+        if discrete:
+            act = np.stack([rng.integers(0, 2, (E, 8)), rng.integers(0, 2, (E, 8)),
+                            rng.integers(0, 50, (E, 8)), np.zeros((E, 8), np.int64)], -1).astype(np.int32)
+            # integer rows: the oracle truncates a random salvo written into
+            # them, as an int ndarray does (the golden discrete fixtures' calls)
+            kinds = np.full((E, 8), _oracle.K_PYINT, np.uint8)
+            at = torch.from_numpy(act).cuda()
+            out = g.step(at)
+        else:
+            act = rng.random((E, 8, 4))
+            kinds = rng.choice([_oracle.K_PYFLOAT, _oracle.K_F32, _oracle.K_F64], (E, 8)).astype(np.uint8)
+            f32 = kinds == _oracle.K_F32
+            act[f32] = act[f32].astype(np.float32)
+            at = torch.from_numpy(act).cuda()
+            out = g.step(at, torch.from_numpy(kinds).cuda())
+        act_after = at.cpu().numpy()
+        ob, orr = out["obs_blue"].cpu().numpy(), out["obs_red"].cpu().numpy()
+        rb, rr = out["rew_blue"].cpu().numpy(), out["rew_red"].cpu().numpy()
+        dn = out["done"].cpu().numpy()
+        for e in range(E):
+            r = oracles[e].step(act[e], kinds[e].astype(np.int32))
+            assert np.array_equal(act_after[e], r["actions_after"].astype(act.dtype)), (s, e, "actions")
+            assert np.array_equal(ob[e], r["obs_blue"].astype(np.float32)), (s, e, "obs_blue")
+            assert np.array_equal(orr[e], r["obs_red"].astype(np.float32)), (s, e, "obs_red")
+            assert np.allclose(rb[e], r["rew_blue"], rtol=0, atol=REW_TOL), (s, e, "rew_blue")
+            assert np.allclose(rr[e], r["rew_red"], rtol=0, atol=REW_TOL), (s, e, "rew_red")
+            assert dn[e] == r["done"], (s, e, "done")
+    g.close()
