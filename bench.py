@@ -48,6 +48,14 @@ def algorithmic_bytes(nb, nr):
     return act + obs + out + 2 * state
 
 
+def survey_bytes(nb, nr):
+    """SURVEY.md §8(d)'s estimate of the same quantity, with a generic 64 B of
+    state per agent and 32 B per env (3 432 B at 4v4); reported beside the
+    build's own minimum for reference."""
+    A = nb + nr
+    return A * 16 + (nb * (4 * nb + 52) + nr * (4 * nr + 52)) * 4 + A * 4 + 8 + 2 * A * 64 + 2 * 32
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -339,6 +347,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_env_step": B,
+                         "survey_bytes_per_env_step": survey_bytes(nb, nr),
+                         "frac_at_survey_bytes": survey_bytes(nb, nr) * E / (kms_mean * 1e-3) / 1e9
+                                                 / HBM_PEAK_GBS,
                          "kernel_ms_mean": kms_mean},
             "cpu_baseline": cpu,
             "err_envs": err,
