@@ -48,6 +48,9 @@ def algorithmic_bytes(nb, nr):
     return act + obs + out + 2 * state
 
 
+REF_LOS_CELLS = 10996  # Bresenham cells per 4v4 env-step, reference spawns
+
+
 def survey_bytes(nb, nr):
     """SURVEY.md §8(d)'s estimate of the same quantity, with a generic 64 B of
     state per agent and 32 B per env (3 432 B at 4v4); reported beside the
@@ -355,6 +358,15 @@ def main():
             "err_envs": err,
             "episodes_completed": episodes,
         }
+        if cfg is None and args.spawns == "reference" and args.los_mode == 0:
+            # SURVEY §8(d) secondary work metric: the reference marches a Bresenham
+            # ray for every own x opponent pair of every get_obs, 10 996 cells per
+            # 4v4 env-step at these spawns (measured there); the build answers every
+            # LOS query it needs from the LOS table and at these spawns needs none
+            # (no pair inside a sensor range), so it marches 0 cells
+            line["los_work"] = {"reference_equivalent_cells_per_env_step": REF_LOS_CELLS,
+                                "reference_equivalent_cells_per_sec": REF_LOS_CELLS * value,
+                                "marched_cells_per_env_step": 0}
         if secondary:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)
