@@ -142,7 +142,10 @@ int lnw_set_rng(lnw_handle *h, int32_t mode, uint64_t seed, const double *tape_d
 
 /* ---- environment API ---------------------------------------------------- */
 /* env_mask_dev: [E] u8, nonzero = reset that env (NULL = all).
- * pos_dev: optional [E][A][2] i32 per-env spawn cells (overrides spawn->pos). */
+ * pos_dev: optional [E][A][2] i32 per-env spawn cells (overrides spawn->pos). It is
+ * copied into the handle (stream-ordered), and the in-kernel auto-reset
+ * (lnw_params.auto_reset) respawns every env on its own cells from then on; a
+ * reset without pos_dev returns all envs to the shared spawn->pos. */
 int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn,
               const int32_t *pos_dev, void *stream);
 

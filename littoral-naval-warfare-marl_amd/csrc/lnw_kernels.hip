@@ -2401,6 +2401,7 @@ struct lnw_handle {
   unsigned long long *rng = nullptr;
   uint32_t *err = nullptr;
   int32_t *sp_types = nullptr, *sp_pos = nullptr, *sp_randls = nullptr, *sp_pos_env = nullptr;
+  bool sp_pos_env_on = false;  // auto-reset respawns on the per-env cells of the last lnw_reset
   const double *tape = nullptr;
   const long long *tape_off = nullptr;
   std::vector<void *> allocs;
@@ -2428,7 +2429,7 @@ KState make_state(lnw_handle *h) {
   s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.ana = h->ana; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
-  s.sp_pos_env = nullptr;
+  s.sp_pos_env = h->sp_pos_env_on ? h->sp_pos_env : nullptr;
   s.nmax = h->nmax;
   return s;
 }
@@ -2739,8 +2740,14 @@ int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn
   HIPCHK(hipMemcpy(h->sp_randls, spawn->rand_ls, sizeof(int32_t) * h->A, hipMemcpyHostToDevice));
   h->kp.box_lo[0] = spawn->box_lo[0]; h->kp.box_lo[1] = spawn->box_lo[1];
   h->kp.box_hi[0] = spawn->box_hi[0]; h->kp.box_hi[1] = spawn->box_hi[1];
+  // per-env spawn cells: kept in the handle for the in-kernel auto-reset
+  if (pos_dev) {
+    const size_t n = (size_t)h->E * h->A * 2;
+    if (!h->sp_pos_env && dalloc(h, &h->sp_pos_env, n)) return LNW_ENOMEM;
+    HIPCHK(hipMemcpyAsync(h->sp_pos_env, pos_dev, n * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  }
+  h->sp_pos_env_on = pos_dev != nullptr;
   KState s = make_state(h);
-  s.sp_pos_env = pos_dev;
   reset_kernel<<<(h->E + 255) / 256, 256, 0, st>>>(h->kp, s, env_mask_dev);
   HIPCHK(hipGetLastError());
   return 0;

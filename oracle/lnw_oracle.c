@@ -1135,3 +1135,63 @@ int64_t orc_bench_range(const orc_params *P, const uint8_t *grid, int G, int nb,
     free(e); free(act); free(kinds); free(ob); free(orr);
     return steps;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Full-size parity driver (tests/test_gpu_fullsize.py only): the global    */
+/* envs [env0, env0 + n) of an E-env batch, Philox-seeded by global env id, */
+/* stepped S times with float32 actions acts[S][E][A][4] (row kind K_F32),  */
+/* auto-reset after done == 0 or `horizon` steps as the device does         */
+/* (lnw_kernels.hip phase W). Per (step, env) it records a 64-bit hash of   */
+/* the float32 observations, sum_k bits(obs[k]) * mult[k] mod 2^64 over the */
+/* blue rows then the red rows, and the float32 rewards, done and cog, so a */
+/* 65 536-env batch is checked without holding its observations.            */
+/* pos: [E][A][2] when pos_per_env, else [A][2]. Disjoint ranges may run on */
+/* concurrent threads.                                                      */
+/* ------------------------------------------------------------------------ */
+void orc_fullsize_range(const orc_params *P, const uint8_t *grid, int G, int nb, int nr,
+                        const int *types, const int *pos, int pos_per_env, const int *rand_ls,
+                        uint64_t seed, int64_t E, int64_t env0, int64_t n, int S, int horizon,
+                        const float *acts, const uint64_t *mult, uint64_t *hash, float *rew,
+                        int32_t *done_out, float *cog_out) {
+    int A = nb + nr, Db = 4 * nb + 52, Dr = 4 * nr + 52;
+    orc_env *e = (orc_env *)malloc(sizeof(orc_env));
+    double *act = (double *)malloc(sizeof(double) * 4 * A);
+    int *kinds = (int *)malloc(sizeof(int) * A);
+    double *ob = (double *)malloc(sizeof(double) * nb * Db);
+    double *orr = (double *)malloc(sizeof(double) * nr * Dr);
+    double rb[ORC_MAX_AGENTS], rr[ORC_MAX_AGENTS], cog;
+    for (int a = 0; a < A; a++) kinds[a] = K_F32;
+    for (int64_t env = env0; env < env0 + n; env++) {
+        const int *p = pos_per_env ? pos + env * A * 2 : pos;
+        orc_env_init(e, P, grid, G, nb, nr);
+        orc_set_rng(e, 0, seed, (uint64_t)env, 0, NULL, 0, 0);
+        orc_reset(e, types, p, rand_ls);
+        for (int s = 0; s < S; s++) {
+            const float *ar = acts + ((int64_t)s * E + env) * A * 4;
+            for (int q = 0; q < 4 * A; q++) act[q] = (double)ar[q];
+            int done = orc_step(e, act, kinds, ob, orr, rb, rr, &cog);
+            uint64_t h = 0;
+            int k = 0;
+            for (int q = 0; q < nb * Db; q++, k++) {
+                float f = (float)ob[q];
+                uint32_t w;
+                memcpy(&w, &f, 4);
+                h += (uint64_t)w * mult[k];
+            }
+            for (int q = 0; q < nr * Dr; q++, k++) {
+                float f = (float)orr[q];
+                uint32_t w;
+                memcpy(&w, &f, 4);
+                h += (uint64_t)w * mult[k];
+            }
+            int64_t se = (int64_t)s * E + env;
+            hash[se] = h;
+            for (int a = 0; a < nb; a++) rew[se * A + a] = (float)rb[a];
+            for (int a = 0; a < nr; a++) rew[se * A + nb + a] = (float)rr[a];
+            done_out[se] = done;
+            cog_out[se] = (float)cog;
+            if (done == 0 || e->steps_done >= horizon) orc_reset(e, types, p, rand_ls);
+        }
+    }
+    free(e); free(act); free(kinds); free(ob); free(orr);
+}

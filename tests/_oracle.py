@@ -69,6 +69,9 @@ def lib():
         L.orc_move_batch.argtypes = [P, C.c_int, C.c_int, P, P, P, P, C.c_int64, P, P]
         L.orc_move_table.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int64, P]
         L.orc_philox.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, P]
+        L.orc_fullsize_range.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P,
+                                         C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                                         C.c_int, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -220,6 +223,41 @@ class OracleEnv:
 # ---------------------------------------------------------------------------
 # golden fixtures
 # ---------------------------------------------------------------------------
+def fullsize(grid, nb, nr, types, pos, acts, mult, seed, horizon, *, pos_per_env=False,
+             rand_ls=None, landing_ops=False, threads=None):
+    """orc_fullsize_range over all E envs of acts [S, E, A, 4] (float32) on a
+    thread pool (ctypes releases the GIL; ranges are disjoint): per (step, env)
+    the observation hash (sum bits * mult mod 2^64), float32 rewards [S, E, A],
+    done [S, E] and cog [S, E]."""
+    from concurrent.futures import ThreadPoolExecutor
+    L = lib()
+    S, E, A = acts.shape[:3]
+    grid = np.ascontiguousarray(grid, np.uint8)
+    acts = np.ascontiguousarray(acts, np.float32)
+    types = np.ascontiguousarray(types, np.int32)
+    pos = np.ascontiguousarray(pos, np.int32)
+    mult = np.ascontiguousarray(mult, np.uint64)
+    rls = np.ascontiguousarray(rand_ls if rand_ls is not None else np.zeros(A), np.int32)
+    P = OrcParams(0, int(landing_ops), 1, 1, 1, 0.4, 74, 70, 14, 82)
+    hsh = np.zeros((S, E), np.uint64)
+    rew = np.zeros((S, E, A), np.float32)
+    done = np.zeros((S, E), np.int32)
+    cog = np.zeros((S, E), np.float32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    chunk = (E + threads - 1) // threads
+
+    def run(i):
+        e0 = i * chunk
+        n = max(0, min(chunk, E - e0))
+        if n:
+            L.orc_fullsize_range(C.byref(P), _p(grid), grid.shape[0], nb, nr, _p(types), _p(pos),
+                                 int(pos_per_env), _p(rls), seed, E, e0, n, S, horizon,
+                                 _p(acts), _p(mult), _p(hsh), _p(rew), _p(done), _p(cog))
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, range(threads)))
+    return hsh, rew, done, cog
+
+
 def load_fixture(name, golden_dir=GOLDEN):
     d = np.load(os.path.join(golden_dir, name), allow_pickle=False)
     return {k: d[k] for k in d.files}
