@@ -92,6 +92,9 @@ def make_game(E, rank, args, spawns, los_mode, move_mode, cfg=None):
                       auto_reset=True, episode_steps=40, los_mode=los_mode, move_mode=move_mode)
         g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc,
                         device=torch.cuda.current_device(), env_id_base=rank * E, seed=1234)
+        # melee: fleets in contact every step -> the contact variant of the
+        # step kernel (lnw_set_variant; identical results)
+        g.set_variant(spawns == "melee")
         box = ((40, 40), (57, 65)) if spawns == "melee" else None
         g.reset(positions=REF_BLUE + REF_RED, box=box)
         return g
@@ -196,6 +199,7 @@ def mappo_rollout(E=32768, T=40, reps=3):
     actor = BatchedActor.for_obs(g.Db).cuda()
     critic = BatchedCritic(g.Db * g.nb).cuda()
     gen = torch.Generator(device="cuda").manual_seed(5)
+    g.set_variant(True)  # scripted red closes in: contact most steps
     r = Rollout(g, actor, critic, steps=T, noise=0.05)
     g.reset(positions=REF_BLUE + REF_RED)
     r.run(generator=gen)
@@ -344,6 +348,7 @@ def main():
                 "agents": "4v4" if cfg is None else f"{nb}v{nr}",
                 "grid": 100 if cfg is None else cfg["G"],
                 "spawns": args.spawns if cfg is None else "box",
+                "kernel_variant": "contact" if (cfg is None and args.spawns == "melee") else "default",
                 "los_mode": args.los_mode,
                 "move_mode": args.move_mode, "parallelism": f"env-shard x{world}",
             },

@@ -190,6 +190,15 @@ int lnw_tlist_cap(lnw_handle *h);
  * a negative LNW_E* code. */
 int lnw_set_epw(lnw_handle *h, int32_t epw);
 
+/* Step-kernel code variant for 2v2 / 3v3 / 4v4 (build-side, no reference
+ * counterpart; results are identical either way). contact = 0 (default): the
+ * variant tuned for envs whose fleets are mostly out of sensor range (the
+ * quiet-workgroup path, BASELINE's reference spawns). contact = 1: get_obs
+ * pair walk as bit masks over registers and two EW bearings per iteration,
+ * faster when fleets are in contact every step (melee, MAPPO rollouts against
+ * a closing red) but slower on the quiet path, which shares the kernel. */
+int lnw_set_variant(lnw_handle *h, int32_t contact);
+
 /* ---- unit kernels (parity tests, standalone use) ------------------------ */
 /* LOS (radar thr = move_thr; EW thr): out[i] = bit0 radar clear | bit1 EW clear
  * for pairs[i] = (x1, y1, x2, y2), traced from (x1,y1) to (x2,y2). */

@@ -343,6 +343,23 @@ __device__ inline double bearing_deg(const KParams &P, const KState &S, int dx, 
   return tab ? S.atan_deg[(dy + R_LOS) * LOS_W + (dx + R_LOS)] : atan2((double)dy, (double)dx) * RAD2DEG;
 }
 
+// bearing_deg split in two: bearing_pre loads unconditionally (the dummy buffer
+// when the table does not apply, so no branch sits between the load and its
+// use), bearing_use returns the table value or falls back to the device atan2
+struct BearPre {
+  double v;
+  bool tab;
+};
+__device__ inline BearPre bearing_pre(const KParams &P, const KState &S, int dx, int dy) {
+  const bool tab = !(P.dbg_skip & 4096) && S.atan_deg && dx >= -R_LOS && dx <= R_LOS &&
+                   dy >= -R_LOS && dy <= R_LOS;
+  const double *p = tab ? S.atan_deg + (dy + R_LOS) * LOS_W + (dx + R_LOS) : (const double *)S.dummy;
+  return {*p, tab};
+}
+__device__ inline double bearing_use(const BearPre &b, int dx, int dy) {
+  return b.tab ? b.v : atan2((double)dy, (double)dx) * RAD2DEG;
+}
+
 // calculate_bearing (combatant.py:249-263) with the gauss draw given
 __device__ inline double ew_bearing(const KParams &P, const KState &S, int xi, int yi, int xj, int yj,
                                     double distortion) {
@@ -638,9 +655,10 @@ __device__ __forceinline__ T rsel(const T (&a)[N], int k) {
 // without storage; the mean of m = n-1 <= 3 fixes is a plain left-to-right sum
 // (np.mean below 8 terms). Fix targets are appended in the order of each
 // opponent's first bearing.
-template <int NOWN, int NOPP>
-__device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const ObsAcc &acc,
-                                    uint32_t bearm) {
+template <int NOWN, int NOPP, bool CW>
+__device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_n,
+                                    uint32_t firstbit, uint32_t bearm,
+                                    const uint32_t (&pp)[NOPP]) {
   static_assert(NOWN < 9, "np.mean pairwise summation starts at 8 terms");
   const KParams &P = X.P;
   const KState &S = X.S;
@@ -660,10 +678,19 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const Ob
   uint16_t *tl = S.tl + (size_t)me * P.T * E + env;
   unsigned long long tq = prof_now(S);
   int tn = 0;
-  for (int q = 0; q < acc.obs_n; q++) {
-    uint32_t pk = COLW(c.observed, q);
-    tl[(size_t)tn * E] = (uint16_t)(pos_x(pk) | (pos_y(pk) << 8));
-    tn++;
+  // observed positions (combatant.py:152-154)
+  if constexpr (CW) {  // one per cell class, in the order of each class's first detecting pair
+    for (uint32_t fb = firstbit; fb; fb &= fb - 1) {
+      const uint32_t pk = rsel(pp, __builtin_ctz(fb) % NOPP);
+      tl[(size_t)tn * E] = (uint16_t)(pos_x(pk) | (pos_y(pk) << 8));
+      tn++;
+    }
+  } else {  // the list the walk built in LDS
+    for (int q = 0; q < obs_n; q++) {
+      uint32_t pk = COLW(c.observed, q);
+      tl[(size_t)tn * E] = (uint16_t)(pos_x(pk) | (pos_y(pk) << 8));
+      tn++;
+    }
   }
   tq = prof_acc(S, 21, tq);
   if (bearm == 0) { COLW(c.tcnt, me) = (uint32_t)tn; return; }
@@ -709,6 +736,66 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const Ob
     }
     fok |= 1u << curj;
   };
+  if constexpr (CW) {
+  // Two bearings per iteration: their gauss draws and tangents are independent
+  // f64 chains the compiler interleaves (with one compute wave per SIMD a single
+  // chain leaves the latency of every dependent op exposed); the fix sums then
+  // take them in order. The table loads of both go first, the rare atan2
+  // fallback after them, so the chains share one basic block.
+  auto setup = [&](int t, int &dx, int &dy, int &j, double &x1, double &y1, int &k) {
+    j = t / NOWN;
+    const int i = t - j * NOWN, b = i * NOPP + j;
+    const uint32_t pi = COLW(c.pos_cur, own0 + i), pj = COLW(c.pos_cur, opp0 + j);
+    dx = pos_x(pj) - pos_x(pi);
+    dy = pos_y(pj) - pos_y(pi);
+    x1 = pos_x(pi);
+    y1 = pos_y(pi);
+    k = __builtin_popcount(bearm & ((1u << b) - 1u));
+  };
+  auto accum = [&](int j, double m, double x1, double y1) {
+    if (j != curj) {
+      flush();
+      curj = j; cnt = 0; zero = false; sumx = sumy = 0.0;
+    }
+    if (cnt > 0 && !zero) {
+      if (mprev - m == 0.0) {
+        zero = true;
+      } else {
+        double x3, y3;
+        fix_pair(mprev, m, xprev, yprev, x1, y1, x3, y3);
+        sumx += x3;
+        sumy += y3;
+      }
+    }
+    cnt++;
+    mprev = m; xprev = x1; yprev = y1;
+  };
+  while (need) {
+    const int t1 = __builtin_ctz(need);
+    need &= need - 1;
+    const bool two = need != 0;
+    const int t2 = two ? __builtin_ctz(need) : t1;
+    if (two) need &= need - 1;
+    int dx1, dy1, j1, k1, dx2, dy2, j2, k2;
+    double x1, y1, x2, y2;
+    setup(t1, dx1, dy1, j1, x1, y1, k1);
+    setup(t2, dx2, dy2, j2, x2, y2, k2);
+    const BearPre b1 = bearing_pre(P, S, dx1, dy1), b2 = bearing_pre(P, S, dx2, dy2);
+    double a1 = b1.v, a2 = b2.v;
+    if (!(b1.tab && b2.tab)) {
+      a1 = bearing_use(b1, dx1, dy1);
+      a2 = bearing_use(b2, dx2, dy2);
+    }
+    const double g1 = X.rng.gauss_at(base + (unsigned long long)k1);
+    const double g2 = X.rng.gauss_at(base + (unsigned long long)k2);
+    // calculate_bearing (combatant.py:249-263)
+    const double br1 = a1 + g1 < 0 ? a1 + g1 + 360.0 : a1 + g1;
+    const double br2 = a2 + g2 < 0 ? a2 + g2 + 360.0 : a2 + g2;
+    const double m1 = tan(br1 * DEG2RAD), m2 = tan(br2 * DEG2RAD);
+    accum(j1, m1, x1, y1);
+    if (two) accum(j2, m2, x2, y2);
+  }
+  } else {
   while (need) {
     const int t = __builtin_ctz(need);
     need &= need - 1;
@@ -738,6 +825,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const Ob
     cnt++;
     mprev = m; xprev = x1; yprev = y1;
   }
+  }
   flush();
   tq = prof_acc(S, 22, tq);
   // fix targets (combatant.py:156-161), opponents in order of their first bearing
@@ -765,7 +853,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const Ob
   prof_acc(S, 23, tq);
 }
 
-// Compile-time ship counts: positions and alive flags of both sides are read
+// Default pair walk (step_kernel CW = false). Compile-time ship counts: positions and alive flags of both sides are read
 // into registers once, the 16 (4v4) distance tests run branch-free, and only
 // pairs inside a sensor range are walked. The walk (pass 1) is integer work: the
 // observed list and which pairs yield an EW bearing; the floating-point part —
@@ -774,7 +862,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, const Ob
 // operands in registers instead of LDS measured slower: the kernel is at 256
 // VGPRs and the extra arrays spill to scratch.)
 template <int NOWN, int NOPP>
-__device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
+__device__ __forceinline__ void get_obs_walk_t(Ctx &X, int me, int own0, int opp0) {
   Cols &c = X.c;
   const int lane = X.lane;
   const int myradar = COLW(c.radar_cur, me);
@@ -830,7 +918,96 @@ __device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
     if (pair_observe(X, xj, yj, rad_ok, close, ew_cand, los, acc)) bearm |= 1u << b;
   }
   prof_acc(X.S, 20, tw);
-  finish_obs_t<NOWN, NOPP>(X, me, own0, opp0, acc, bearm);
+  const uint32_t nopp[NOPP] = {};
+  finish_obs_t<NOWN, NOPP, false>(X, me, own0, opp0, acc.obs_n, 0u, bearm, nopp);
+}
+
+// Contact variant (step_kernel CW = true, lnw_set_variant): the pair walk of
+// get_obs (combatant.py:106-124) as
+// bit masks. Positions, types, alive flags and the opponents' radar states are
+// read into registers once; every (own i, opponent j) pair's conditions are
+// evaluated independently (LOS bits from los_prefetch_t), giving
+//   D  = pairs that detect (radar or close, radar LOS clear),
+//   EW = pairs that are EW candidates with radar and EW LOS clear.
+// The reference walks pairs in index order (i outer, j inner) appending each
+// detected opponent's cell to `observed` unless a cell-mate is already there,
+// and takes a bearing when an EW pair's opponent cell is not yet observed
+// (after the pair's own append). With f = the first D pair over the opponents
+// sharing j's cell, the observed list is the set of those f in increasing
+// order, and pair b of column j yields a bearing iff b is in EW and b < f.
+// Bearings, gauss draws and fixes then run in finish_obs_t.
+template <int NOWN, int NOPP>
+__device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp0) {
+  static_assert(NOWN * NOPP <= 16, "pair masks are 16 bits");
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const int myradar = COLW(c.radar_cur, me);
+  uint32_t po[NOWN], pp[NOPP];
+  uint32_t tbits = 0;  // 2 bits per ship type: own ships at bit 2i, opponents at 2(NOWN+j)
+  uint32_t amask = 0, orad = 0, onew = 0;
+#pragma unroll
+  for (int i = 0; i < NOWN; i++) {
+    po[i] = COLW(c.pos_cur, own0 + i);
+    tbits |= (uint32_t)COLB(c.type, own0 + i) << (2 * i);
+    amask |= (COLB(c.alive0, own0 + i) ? 1u : 0u) << i;
+    // own ship i stands on its new cell once its turn has come and it moved
+    onew |= ((own0 + i <= me) && (COLW(c.pos_new, own0 + i) & 0x80000000u) ? 1u : 0u) << i;
+  }
+#pragma unroll
+  for (int j = 0; j < NOPP; j++) {
+    pp[j] = COLW(c.pos_cur, opp0 + j);
+    tbits |= (uint32_t)COLB(c.type, opp0 + j) << (2 * (NOWN + j));
+    amask |= (COLB(c.alive0, opp0 + j) ? 1u : 0u) << (NOWN + j);
+    orad |= (COLW(c.radar_cur, opp0 + j) == 1 ? 1u : 0u) << j;
+  }
+  const unsigned long long tw = prof_now(X.S);
+  const double duct = X.duct();
+  const uint64_t lbits = X.lpre[own0 != 0];
+  uint32_t detm = 0, ewm = 0;
+#pragma unroll
+  for (int i = 0; i < NOWN; i++)
+#pragma unroll
+    for (int j = 0; j < NOPP; j++) {
+      const int b = i * NOPP + j;
+      const int dx = pos_x(pp[j]) - pos_x(po[i]), dy = pos_y(pp[j]) - pos_y(po[i]);
+      const int d2 = dx * dx + dy * dy;
+      const bool in = ((amask >> i) & (amask >> (NOWN + j)) & 1u) && d2 < X.r2max;
+      const int ti = (tbits >> (2 * i)) & 3u, tj = (tbits >> (2 * (NOWN + j))) & 3u;
+      const int rr = radar_r(X.P, duct, ti, tj), re = ew_r(X.P, duct, ti, tj);
+      const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
+      const bool ew_cand = d2 < re * re && ((orad >> j) & 1u);
+      uint32_t los = 0;
+      if (X.pre) {
+        los = (uint32_t)(lbits >> ((b * 2 + ((onew >> i) & 1u)) * 2)) & 3u;
+      } else if (in && (rad_ok || close || ew_cand)) {  // LOS result would be unused otherwise
+        los = los_q(X.P, X.S, X.mask, pos_x(po[i]), pos_y(po[i]), pos_x(pp[j]), pos_y(pp[j]));
+      }
+      detm |= (in && (rad_ok || close) && (los & 1u)) ? 1u << b : 0u;
+      ewm |= (in && ew_cand && (los & 3u) == 3u) ? 1u << b : 0u;
+    }
+  uint32_t colj = 0;  // bits of opponent 0's column
+#pragma unroll
+  for (int i = 0; i < NOWN; i++) colj |= 1u << (i * NOPP);
+  uint32_t firstbit = 0, bearm = 0;  // bit b: pair b appends to observed / takes a bearing
+#pragma unroll
+  for (int j = 0; j < NOPP; j++) {
+    uint32_t cls = 0;  // columns of the opponents on j's cell (observed is de-duplicated by cell)
+#pragma unroll
+    for (int k = 0; k < NOPP; k++) cls |= pp[k] == pp[j] ? colj << k : 0u;
+    const uint32_t dc = detm & cls;
+    const uint32_t f = dc ? 1u << __builtin_ctz(dc) : 0u;
+    firstbit |= f;
+    bearm |= ewm & (colj << j) & (f ? f - 1u : 0xffffffffu);
+  }
+  prof_acc(X.S, 20, tw);
+  finish_obs_t<NOWN, NOPP, true>(X, me, own0, opp0, 0, firstbit, bearm, pp);
+}
+
+// get_obs for compile-time ship counts: CW selects the contact variant
+template <int NOWN, int NOPP, bool CW>
+__device__ __forceinline__ void get_obs_t(Ctx &X, int me, int own0, int opp0) {
+  if constexpr (CW) get_obs_mask_t<NOWN, NOPP>(X, me, own0, opp0);
+  else get_obs_walk_t<NOWN, NOPP>(X, me, own0, opp0);
 }
 
 // Every LOS query get_obs can make during this step's agent loop, loaded in one
@@ -1919,7 +2096,7 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // observation copy-out); NB = NR = 0: runtime counts from P.
 // NB/NR > 0 run two waves per workgroup: wave 0 steps the envs, wave 1 emits
 // the observation rows (emit_wave_t).
-template <int NB, int NR>
+template <int NB, int NR, bool CW = false>
 __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
@@ -2089,8 +2266,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       t0 = prof_now(S);
       if (al && !(P.dbg_skip & 128)) {
         if constexpr (ST) {
-          if (!side) get_obs_t<NB, NR>(X, a, 0, NB);
-          else get_obs_t<NR, NB>(X, a, NB, 0);
+          if (!side) get_obs_t<NB, NR, CW>(X, a, 0, NB);
+          else get_obs_t<NR, NB, CW>(X, a, NB, 0);
         } else {
           get_obs_dev(X, a);
         }
@@ -2391,6 +2568,7 @@ struct lnw_handle {
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
   bool prof = false, force_generic = false;
+  bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -2775,14 +2953,15 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
     s.prof = h->d_prof;
   }
   bool generic = h->force_generic;
-#define LNW_STEP(NB_, NR_)                                                                       \
-  step_kernel<NB_, NR_><<<grid, dim3(NB_ > 0 && EPW == WAVE ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
+#define LNW_STEP(NB_, NR_, CW_)                                                                  \
+  step_kernel<NB_, NR_, CW_><<<grid, dim3(NB_ > 0 && EPW == WAVE ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
                                                  done_dev, cog_dev)
-  if (!generic && h->nb == 4 && h->nr == 4) LNW_STEP(4, 4);
-  else if (!generic && h->nb == 3 && h->nr == 3) LNW_STEP(3, 3);
-  else if (!generic && h->nb == 2 && h->nr == 2) LNW_STEP(2, 2);
-  else LNW_STEP(0, 0);
+  const bool cw = h->contact;
+  if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true); else LNW_STEP(4, 4, false); }
+  else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true); else LNW_STEP(3, 3, false); }
+  else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true); else LNW_STEP(2, 2, false); }
+  else LNW_STEP(0, 0, false);
 #undef LNW_STEP
   HIPCHK(hipGetLastError());
   if (s.prof) prof_report(h, st, (int)grid.x);
@@ -2825,6 +3004,12 @@ int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbyte
 }
 
 int lnw_tlist_cap(lnw_handle *h) { return h ? h->T : LNW_EINVAL; }
+
+int lnw_set_variant(lnw_handle *h, int32_t contact) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  h->contact = contact != 0;
+  return 0;
+}
 
 int lnw_set_epw(lnw_handle *h, int32_t epw) {
   if (!h) return fail(LNW_EINVAL, "null handle");

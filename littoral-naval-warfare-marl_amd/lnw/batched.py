@@ -111,6 +111,14 @@ class BatchedGame:
         self.epw = rc
         return rc
 
+    def set_variant(self, contact):
+        """Step-kernel code variant (lnw_set_variant): contact=True for workloads
+        whose fleets are in sensor range most steps (melee spawns, MAPPO rollouts
+        against a closing red); False (default) for mostly quiet ones. Results do
+        not depend on it."""
+        check(self.L.lnw_set_variant(self.h, int(bool(contact))))
+        self.contact = bool(contact)
+
     def set_rng(self, seed):
         """Production RNG: Philox4x32-10 keyed by (seed, global env id)."""
         self._tape = None

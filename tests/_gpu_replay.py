@@ -20,7 +20,7 @@ def scenario_from_meta(meta, **over):
                     red_aggression=F["RED_AGGRESSION"], **over)
 
 
-def replay_gpu(fx, grids, los_mode=0, move_mode=0):
+def replay_gpu(fx, grids, los_mode=0, move_mode=0, contact=False):
     """Yields (step index s, list of (env, fixture row)) plus the game and the
     output dict after each batched step. Before each step, if the fixture was
     recorded with caller-side observes, yields ('observe', ...) first."""
@@ -34,6 +34,7 @@ def replay_gpu(fx, grids, los_mode=0, move_mode=0):
     names = {0: "small", 1: "large", 2: "ls"}
     g = BatchedGame(E, [names[t] for t in types[:nb]], [names[t] for t in types[nb:]],
                     scenario=sc, grid=grid)
+    g.set_variant(contact)
     # tape slices, one per env
     tapes = [fx["tape"][em["tape_start"]:em["tape_end"]] for em in eps]
     offs = np.concatenate([[0], np.cumsum([len(t) for t in tapes])]).astype(np.int64)

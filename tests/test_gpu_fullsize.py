@@ -91,7 +91,8 @@ def test_fullsize_config3_reference_spawns():
     assert (gpu[2][39] == 1).all()  # horizon reached, envs reset in-kernel after step 40
 
 
-def test_fullsize_config2_contact_spawns():
+@pytest.mark.parametrize("contact", [False, True])
+def test_fullsize_config2_contact_spawns(contact):
     """Config 2 size (4 096 4v4 envs) with the sides 10-40 cells apart, so
     firing, hits, EW bearings and fixes happen every step (phase S workgroups),
     45 steps, every env vs the oracle."""
@@ -102,6 +103,7 @@ def test_fullsize_config2_contact_spawns():
     pos = _water_positions(grid, E, [(30, 45, 40, 60)] * 4 + [(55, 70, 45, 65)] * 4, seed=3)
     sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40)
     g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grid, seed=seed)
+    g.set_variant(contact)  # both step-kernel variants (lnw_set_variant)
     g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
     acts = np.random.default_rng(6).random((S, E, 8, 4), dtype=np.float32)
     mult = _mult(4 * 68 + 4 * 68, seed=7)

@@ -239,14 +239,14 @@ def test_device_sqrt_is_correctly_rounded(lib, grids):
 # ---------------------------------------------------------------------------
 # full episodes, tape mode
 # ---------------------------------------------------------------------------
-def _cmp_episode(name, grids, los_mode, move_mode):
+def _cmp_episode(name, grids, los_mode, move_mode, contact=False):
     from _gpu_replay import replay_gpu
     fx = load_fixture(name)
     meta = episode_meta(fx)
     cnt, xy = fx["tl_cnt"], fx["tl_xy"]
     offs = np.concatenate([[0], np.cumsum(cnt.reshape(-1))])
     checked = 0
-    for kind, info, g, res in replay_gpu(fx, grids, los_mode, move_mode):
+    for kind, info, g, res in replay_gpu(fx, grids, los_mode, move_mode, contact):
         if kind == "reset":
             ds = g.env_state()["ducting"]
             for e, em in enumerate(meta["episodes"]):
@@ -314,6 +314,13 @@ def _cmp_episode(name, grids, los_mode, move_mode):
 @pytest.mark.parametrize("name", EPISODES)
 def test_episode_gpu_tape(name, grids):
     _cmp_episode(name, grids, los_mode=0, move_mode=0)
+
+
+@pytest.mark.parametrize("name", EPISODES)
+def test_episode_gpu_tape_contact_variant(name, grids):
+    """Every golden episode through the contact variant of the step kernel
+    (lnw_set_variant: bit-mask pair walk, two bearings per iteration)."""
+    _cmp_episode(name, grids, los_mode=0, move_mode=0, contact=True)
 
 
 @pytest.mark.parametrize("name", ["ep_4v4_melee_f64.npz", "ep_4v4_split_f64.npz",
@@ -396,8 +403,8 @@ def _melee_positions(grid, E, nb, nr, seed, box_b=(30, 45, 40, 60), box_r=(55, 7
                      [wr[i] for i in rng.integers(0, len(wr), nr)] for _ in range(E)], np.int32)
 
 
-@pytest.mark.parametrize("epw", [64, 16, 1])
-def test_philox_4v4_vs_oracle_launch_shapes(grids, epw):
+@pytest.mark.parametrize("epw,contact", [(64, False), (16, False), (1, False), (64, True), (16, True)])
+def test_philox_4v4_vs_oracle_launch_shapes(grids, epw, contact):
     """4v4 split spawns (fire, EW bearings and fixes happen) in production
     (Philox) mode, 128 envs, with the step launched at 64 / 16 / 1 envs per
     workgroup (64: the two-wave emission path; 16, 1: phase O after phase S),
@@ -410,6 +417,7 @@ def test_philox_4v4_vs_oracle_launch_shapes(grids, epw):
     g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
                     grid=grid, seed=11)
     assert g.set_epw(epw) == epw
+    g.set_variant(contact)
     pos = _melee_positions(grid, E, 4, 4, seed=epw)
     g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
     oracles = []
