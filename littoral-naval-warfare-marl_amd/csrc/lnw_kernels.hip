@@ -389,6 +389,37 @@ __device__ inline void pair_after_los(Ctx &X, int i, int jj, int xi, int yi, int
   }
 }
 
+// pair_after_los for the runtime-size walk (get_obs_dev): `obsm` bit k is set
+// once opponent k's cell is in `observed`, so the de-duplication is one bit test
+// instead of a scan of the LDS list per pair. Cells do not change during a
+// get_obs call, so bit k <=> pos(k) in observed, as the reference's test.
+__device__ inline void pair_after_los_m(Ctx &X, int i, int jj, int opp0, int nopp, int xi, int yi,
+                                        int xj, int yj, bool rad_ok, bool close, bool ew_cand,
+                                        uint32_t los, ObsAcc &acc, uint64_t &obsm) {
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  if (!(los & 1u)) return;
+  bool seen = (obsm >> jj) & 1u;
+  if ((rad_ok || close) && !seen) {
+    const uint32_t pk = pack_pos(xj, yj);
+    COLW(c.observed, acc.obs_n) = pk;
+    acc.obs_n++;
+    for (int k = 0; k < nopp; k++)  // every opponent on this cell is now observed
+      if (COLW(c.pos_cur, opp0 + k) == pk) obsm |= 1ull << k;
+    seen = true;
+  }
+  if (ew_cand && (los & 2u) && !seen) {
+    const double bearing = ew_bearing(X.P, S, xi, yi, xj, yj, X.rng.gauss());
+    int k = COLB(c.bcnt, jj);
+    if (k == 0) { COLB(c.border, acc.norder) = (uint8_t)jj; acc.norder++; }
+    size_t slot = (size_t)(jj * S.nmax + k) * X.E + X.env;
+    S.bear_val[slot] = bearing;
+    S.bear_ship[slot] = (uint8_t)i;
+    COLB(c.bcnt, jj) = (uint8_t)(k + 1);
+  }
+}
+
 // Target list (combatant.py:152-161): observed positions first, then every EW
 // fix (combatant.py:128-150) landing within 2 cells of a live opponent.
 // Mean of the consecutive-pair EW fixes of opponent jj's n bearings
@@ -564,6 +595,16 @@ __device__ inline void finish_obs(Ctx &X, int me, int opp0, int opp1, const ObsA
 }
 
 
+// Select a[k] of a small register array without indexing (which would move
+// the array to scratch).
+template <int N, class T>
+__device__ __forceinline__ T rsel(const T (&a)[N], int k) {
+  T v = a[0];
+#pragma unroll
+  for (int q = 1; q < N; q++) v = k == q ? a[q] : v;
+  return v;
+}
+
 // get_obs sensor fusion (combatant.py:90-161 / landingship.py:94-165) for
 // runtime ship counts: refreshes agent me's target list (observation floats are
 // written in phase O).
@@ -579,9 +620,11 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   const int nopp = opp1 - opp0, npair = (own1 - own0) * nopp;
   const int myradar = COLW(c.radar_cur, me);
   ObsAcc acc{0, 0};
+  uint64_t obsm = 0;  // opponents whose cell is already observed
   for (int q = 0; q < nopp; q++) COLB(c.bcnt, q) = 0;
   // pairs (i outer, j inner) in chunks of 16: the sensor tests of a chunk, then
   // its LOS table words loaded together, then the chunk walked in order
+  const unsigned long long tw = prof_now(S);
 #pragma unroll 1
   for (int b0 = 0; b0 < npair; b0 += 16) {
     uint32_t radm = 0, closem = 0, ewm = 0, tabm = 0, marchm = 0;
@@ -629,22 +672,15 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
       const int xi = pos_x(pi), yi = pos_y(pi), xj = pos_x(pj), yj = pos_y(pj);
       const uint32_t los = (tabm >> u) & 1u ? (losb >> (2 * u)) & 3u
                                             : los_q(P, S, X.mask, xi, yi, xj, yj);
-      pair_after_los(X, i, j - opp0, xi, yi, xj, yj, (radm >> u) & 1u, (closem >> u) & 1u,
-                     (ewm >> u) & 1u, los, acc);
+      pair_after_los_m(X, i, j - opp0, opp0, nopp, xi, yi, xj, yj, (radm >> u) & 1u,
+                       (closem >> u) & 1u, (ewm >> u) & 1u, los, acc, obsm);
     }
   }
+  const unsigned long long tf = prof_acc(S, 20, tw);
   finish_obs<16, false>(X, me, opp0, opp1, acc);
+  prof_acc(S, 22, tf);
 }
 
-// Select a[k] of a small register array without indexing (which would move
-// the array to scratch).
-template <int N, class T>
-__device__ __forceinline__ T rsel(const T (&a)[N], int k) {
-  T v = a[0];
-#pragma unroll
-  for (int q = 1; q < N; q++) v = k == q ? a[q] : v;
-  return v;
-}
 
 // Target list of a templated get_obs (combatant.py:128-161) from pass 1's
 // observed list and bearing requests. Bearing k of the call (pair
