@@ -127,13 +127,16 @@ def test_actor_device_matches_reference():
     np.testing.assert_allclose(lp.cpu().numpy(), gold["tr_lp"], rtol=0, atol=1e-4)
 
 
-def test_rollout_graph_replay_matches_eager():
+@pytest.mark.parametrize("E,T,contact", [(512, 10, False), (32768, 40, True)])
+def test_rollout_graph_replay_matches_eager(E, T, contact):
     """Rollout.capture / replay (HIP graph of a whole rollout) against the eager
-    run from the same env state and generator state: identical buffers."""
+    run from the same env state and generator state: identical buffers. The
+    second case is config 5's full size (32 768 envs, 40-step rollout, the
+    contact kernel variant the config-5 bench line uses)."""
     from lnw import _abi
     from lnw.rollout import BatchedActor, BatchedCritic, Rollout
-    E, T = 512, 10
     g = _game(E, seed=5)
+    g.set_variant(contact)
     torch.manual_seed(2)
     actor = BatchedActor.for_obs(g.Db).cuda()
     critic = BatchedCritic(g.Db * g.nb).cuda()
