@@ -629,12 +629,15 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   for (int b0 = 0; b0 < npair; b0 += 16) {
     uint32_t radm = 0, closem = 0, ewm = 0, tabm = 0, marchm = 0;
     uint32_t wi[16];
+    // (i, j) of the chunk's pairs stepped incrementally: one division per chunk
+    int ic = own0 + b0 / nopp, jc = opp0 + b0 % nopp;
 #pragma unroll
     for (int u = 0; u < 16; u++) {
       wi[u] = 0;
       const int b = b0 + u;
+      const int i = ic, j = jc;
+      if (++jc == opp1) { jc = opp0; ++ic; }
       if (b >= npair) continue;
-      const int i = own0 + b / nopp, j = opp0 + b % nopp;
       if (!COLB(c.alive0, i) || !COLB(c.alive0, j)) continue;
       const uint32_t pi = COLW(c.pos_cur, i), pj = COLW(c.pos_cur, j);
       const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
