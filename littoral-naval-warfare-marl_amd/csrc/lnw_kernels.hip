@@ -622,6 +622,18 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   ObsAcc acc{0, 0};
   uint64_t obsm = 0;  // opponents whose cell is already observed
   for (int q = 0; q < nopp; q++) COLB(c.bcnt, q) = 0;
+  // radar / EW ranges of this env's duct for every (own mast class, opponent
+  // type) once per call, selected per pair instead of recomputed in f64
+  const double duct = X.duct();
+  int rr_t[2][3], re_t[2][3];
+#pragma unroll
+  for (int mi = 0; mi < 2; mi++)
+#pragma unroll
+    for (int tj = 0; tj < 3; tj++) {
+      const int ti = mi ? T_LARGE : T_SMALL;
+      rr_t[mi][tj] = radar_r(P, duct, ti, tj);
+      re_t[mi][tj] = ew_r(P, duct, ti, tj);
+    }
   // pairs (i outer, j inner) in chunks of 16: the sensor tests of a chunk, then
   // its LOS table words loaded together, then the chunk walked in order
   const unsigned long long tw = prof_now(S);
@@ -643,8 +655,12 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
       const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
       const int d2 = dx * dx + dy * dy;
       if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
-      const int ti = COLB(c.type, i), tj = COLB(c.type, j);
-      const int rr = radar_r(P, X.duct(), ti, tj), re = ew_r(P, X.duct(), ti, tj);
+      const int mi = mast_cls(COLB(c.type, i)), tj = COLB(c.type, j);
+      const int rr0 = tj == T_SMALL ? rr_t[0][0] : (tj == T_LARGE ? rr_t[0][1] : rr_t[0][2]);
+      const int rr1 = tj == T_SMALL ? rr_t[1][0] : (tj == T_LARGE ? rr_t[1][1] : rr_t[1][2]);
+      const int re0 = tj == T_SMALL ? re_t[0][0] : (tj == T_LARGE ? re_t[0][1] : re_t[0][2]);
+      const int re1 = tj == T_SMALL ? re_t[1][0] : (tj == T_LARGE ? re_t[1][1] : re_t[1][2]);
+      const int rr = mi ? rr1 : rr0, re = mi ? re1 : re0;
       const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
       const bool ew_cand = d2 < re * re && COLW(c.radar_cur, j) == 1;
       if (!(rad_ok || close || ew_cand)) continue;  // LOS result would be unused
