@@ -642,20 +642,35 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
     uint32_t radm = 0, closem = 0, ewm = 0, tabm = 0, marchm = 0;
     uint32_t wi[16];
     // (i, j) of the chunk's pairs stepped incrementally: one division per chunk
+    // (wave-uniform); the own ship's alive flag, cell and mast class are loaded
+    // when i changes, not per pair
     int ic = own0 + b0 / nopp, jc = opp0 + b0 % nopp;
+    bool al_i = COLB(c.alive0, ic);
+    uint32_t pi_c = COLW(c.pos_cur, ic);
+    int mi_c = mast_cls(COLB(c.type, ic));
 #pragma unroll
     for (int u = 0; u < 16; u++) {
       wi[u] = 0;
       const int b = b0 + u;
-      const int i = ic, j = jc;
-      if (++jc == opp1) { jc = opp0; ++ic; }
+      const int j = jc;
+      const bool ali = al_i;
+      const uint32_t pi = pi_c;
+      const int mi = mi_c;
+      if (++jc == opp1) {
+        jc = opp0;
+        if (++ic < own1) {
+          al_i = COLB(c.alive0, ic);
+          pi_c = COLW(c.pos_cur, ic);
+          mi_c = mast_cls(COLB(c.type, ic));
+        }
+      }
       if (b >= npair) continue;
-      if (!COLB(c.alive0, i) || !COLB(c.alive0, j)) continue;
-      const uint32_t pi = COLW(c.pos_cur, i), pj = COLW(c.pos_cur, j);
+      if (!ali || !COLB(c.alive0, j)) continue;
+      const uint32_t pj = COLW(c.pos_cur, j);
       const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
       const int d2 = dx * dx + dy * dy;
       if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
-      const int mi = mast_cls(COLB(c.type, i)), tj = COLB(c.type, j);
+      const int tj = COLB(c.type, j);
       const int rr0 = tj == T_SMALL ? rr_t[0][0] : (tj == T_LARGE ? rr_t[0][1] : rr_t[0][2]);
       const int rr1 = tj == T_SMALL ? rr_t[1][0] : (tj == T_LARGE ? rr_t[1][1] : rr_t[1][2]);
       const int re0 = tj == T_SMALL ? re_t[0][0] : (tj == T_LARGE ? re_t[0][1] : re_t[0][2]);
