@@ -40,6 +40,7 @@
  *                       float64 value; dead slots are zeros)
  *  rew_blue  [E][nb] f32, rew_red [E][nr] f32, done [E] i32 (1 running, 0 over),
  *  cog       [E] f32 (NaN where the reference returns None)
+ *  rew_* and cog are float64 instead after lnw_set_reward_dtype(h, 1)
  */
 #ifndef LNW_H
 #define LNW_H
@@ -51,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LNW_ABI_VERSION 2
+#define LNW_ABI_VERSION 3
 
 /* status codes */
 #define LNW_OK 0
@@ -198,6 +199,12 @@ int lnw_set_epw(lnw_handle *h, int32_t epw);
  * faster when fleets are in contact every step (melee, MAPPO rollouts against
  * a closing red) but slower on the quiet path, which shares the kernel. */
 int lnw_set_variant(lnw_handle *h, int32_t contact);
+
+/* Reward / cog output type of lnw_step. f64 = 0 (default): rew_blue, rew_red and
+ * cog are float32 arrays; f64 = 1: they are float64 arrays (pass double* cast to
+ * float*), the exact values the reference returns as Python floats
+ * (game.py:214-295, 507-525) rather than their float32 rounding. */
+int lnw_set_reward_dtype(lnw_handle *h, int32_t f64);
 
 /* ---- unit kernels (parity tests, standalone use) ------------------------ */
 /* LOS (radar thr = move_thr; EW thr): out[i] = bit0 radar clear | bit1 EW clear

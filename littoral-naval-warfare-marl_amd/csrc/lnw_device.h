@@ -37,6 +37,7 @@ struct KParams {
   int E, nb, nr, A, G, T, W16;
   int rng_mode;
   int act_dtype;
+  int rew_f64;        // lnw_set_reward_dtype: rew_blue/rew_red are float64 arrays
   long long env_base;
   unsigned long long seed;
   double red_aggression;

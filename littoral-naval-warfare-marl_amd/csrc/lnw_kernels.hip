@@ -1924,14 +1924,28 @@ __device__ __forceinline__ bool move_batch_t(const KParams &P, const KState &S, 
     const int sx = pos_x(p), sy = pos_y(p);
     const int t = c.type[a * PADB + e];
     uint32_t target = p;  // no candidate
-    if constexpr (DT == LNW_ACT_I32) {
-      c.act0[a * PAD + e] = (double)vi[k].x;
-      c.act1[a * PAD + e] = (double)vi[k].y;
+    // DISCRETE rows (value_to_coordinates, combatant.py:689-704): an int32
+    // buffer is an integer ndarray; a float64 buffer holds the Python ints of a
+    // list of lists (ddqn.py:396), whose salvo entry game.py:379 may turn into a
+    // float in place
+    bool disc = DT == LNW_ACT_I32;
+    if constexpr (DT == LNW_ACT_F64) disc = P.discrete != 0;
+    if (disc) {
+      int mv = 0;
+      if constexpr (DT == LNW_ACT_I32) {
+        c.act0[a * PAD + e] = (double)vi[k].x;
+        c.act1[a * PAD + e] = (double)vi[k].y;
+        mv = vi[k].z;
+      } else if constexpr (DT == LNW_ACT_F64) {
+        c.act0[a * PAD + e] = v01[k].x;
+        c.act1[a * PAD + e] = v01[k].y;
+        mv = (int)v23[k].x;
+      }
       c.akind[a * PADB + e] = K_PYINT;
-      const int x = floordiv7(vi[k].z), y = pymod7(vi[k].z);
+      const int x = floordiv7(mv), y = pymod7(mv);
       if (0 <= sx - 3 + x && sx - 3 + x < P.G && 0 <= sy - 3 + y && sy - 3 + y < P.G)
         target = pack_pos(sx - 3 + x, sy - 3 + y) | 0x40000000u;
-    } else {
+    } else if constexpr (DT != LNW_ACT_I32) {
       double a2, a3;
       int kind;
       if constexpr (DT == LNW_ACT_F32) {
@@ -2057,7 +2071,7 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
   const long long E = P.E;
   const int nr = A - nb;
   int done = 1;
-  float cog = NAN;
+  double cog = NAN;
   // ---- tail (game.py:409-520) -------------------------------------------
   int nbl = ev[0] - N.cnt[0];
   int nrl = ev[1] - N.cnt[1];
@@ -2124,15 +2138,25 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
   ev[2] = steps_env;
   if (nbp > 0 && nrp > 0) {
     double bx = (double)bsx / nbp, by = (double)bsy / nbp, rx = (double)rsx / nrp, ry = (double)rsy / nrp;
-    cog = (float)sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
+    cog = sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
   }
   // outputs
-  for (int a = 0; a < nb; a++)
-    if (rew_b) rew_b[(size_t)env * nb + a] = (float)COLW(c.reward, a);
-  for (int a = 0; a < nr; a++)
-    if (rew_r) rew_r[(size_t)env * nr + a] = (float)COLW(c.reward, nb + a);
+  // float32 values by default; float64 (the reference's Python floats) when
+  // lnw_set_reward_dtype asked for it
+  if (P.rew_f64) {
+    for (int a = 0; a < nb; a++)
+      if (rew_b) ((double *)rew_b)[(size_t)env * nb + a] = COLW(c.reward, a);
+    for (int a = 0; a < nr; a++)
+      if (rew_r) ((double *)rew_r)[(size_t)env * nr + a] = COLW(c.reward, nb + a);
+    if (cog_out) ((double *)cog_out)[env] = cog;
+  } else {
+    for (int a = 0; a < nb; a++)
+      if (rew_b) rew_b[(size_t)env * nb + a] = (float)COLW(c.reward, a);
+    for (int a = 0; a < nr; a++)
+      if (rew_r) rew_r[(size_t)env * nr + a] = (float)COLW(c.reward, nb + a);
+    if (cog_out) cog_out[env] = (float)cog;
+  }
   if (done_out) done_out[env] = done;
-  if (cog_out) cog_out[env] = cog;
   prof_stamp(S, 2);
   // ---- phase W: store state (alive updated by the neutralized lists) --
   bool do_reset = P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
@@ -2940,9 +2964,10 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     size_t need = step_lds_bytes(h) + 1024;
     if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     if (need > 64 * 1024) {
-      const void *ks[5] = {(const void *)step_kernel<0, 0>, (const void *)step_kernel<2, 2>,
-                           (const void *)step_kernel<3, 3>, (const void *)step_kernel<4, 4>,
-                           (const void *)observe_kernel};
+      const void *ks[8] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
+                           (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
+                           (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
+                           (const void *)step_kernel<4, 4, true>, (const void *)observe_kernel};
       for (const void *kk : ks)
         HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
     }
@@ -3008,8 +3033,10 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
   if (action_dtype != LNW_ACT_F32 && action_dtype != LNW_ACT_F64 && action_dtype != LNW_ACT_I32)
     return fail(LNW_EINVAL, "bad action dtype");
-  if ((action_dtype == LNW_ACT_I32) != (h->params.discrete != 0))
-    return fail(LNW_EINVAL, "integer actions go with DISCRETE mode and only with it");
+  if (action_dtype == LNW_ACT_I32 && !h->params.discrete)
+    return fail(LNW_EINVAL, "integer actions go with DISCRETE mode only");
+  if (action_dtype == LNW_ACT_F32 && h->params.discrete)
+    return fail(LNW_EINVAL, "DISCRETE mode takes int32 (ndarray) or float64 (list rows) actions");
   KParams k = h->kp;
   k.act_dtype = action_dtype;
   k.dbg_skip = h->dbg_skip;
@@ -3074,6 +3101,12 @@ int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbyte
 }
 
 int lnw_tlist_cap(lnw_handle *h) { return h ? h->T : LNW_EINVAL; }
+
+int lnw_set_reward_dtype(lnw_handle *h, int32_t f64) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  h->kp.rew_f64 = f64 != 0;
+  return 0;
+}
 
 int lnw_set_variant(lnw_handle *h, int32_t contact) {
   if (!h) return fail(LNW_EINVAL, "null handle");

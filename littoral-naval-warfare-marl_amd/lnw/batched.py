@@ -59,7 +59,7 @@ def _ptr(t):
 
 class BatchedGame:
     def __init__(self, n_envs, blue_types, red_types, scenario=None, device=0, env_id_base=0,
-                 grid=None, seed=0):
+                 grid=None, seed=0, reward_dtype=torch.float32):
         self.L = _abi.load()
         self.sc = scenario or Scenario()
         self.E = int(n_envs)
@@ -85,10 +85,16 @@ class BatchedGame:
         dev = self.device
         self.obs_blue = torch.zeros((self.E, self.nb, self.Db), dtype=torch.float32, device=dev)
         self.obs_red = torch.zeros((self.E, self.nr, self.Dr), dtype=torch.float32, device=dev)
-        self.rew_blue = torch.zeros((self.E, self.nb), dtype=torch.float32, device=dev)
-        self.rew_red = torch.zeros((self.E, self.nr), dtype=torch.float32, device=dev)
+        # rewards and cog: float32, or float64 (the reference's Python floats,
+        # game.py:522-525) through lnw_set_reward_dtype
+        if reward_dtype not in (torch.float32, torch.float64):
+            raise TypeError("reward_dtype must be torch.float32 or torch.float64")
+        rdt = reward_dtype
+        check(self.L.lnw_set_reward_dtype(self.h, int(rdt == torch.float64)))
+        self.rew_blue = torch.zeros((self.E, self.nb), dtype=rdt, device=dev)
+        self.rew_red = torch.zeros((self.E, self.nr), dtype=rdt, device=dev)
         self.done = torch.ones((self.E,), dtype=torch.int32, device=dev)
-        self.cog = torch.zeros((self.E,), dtype=torch.float32, device=dev)
+        self.cog = torch.zeros((self.E,), dtype=rdt, device=dev)
         self._spawn = None
         self._ana = None
         # step() hot path: output pointers and the accepted action layout, cached

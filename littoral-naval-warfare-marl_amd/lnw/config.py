@@ -12,6 +12,7 @@ from ._abi import Params
 class Scenario:
     discrete: bool = False          # overall.discrete
     landing_ops: bool = True        # overall.landing_ops
+    coa_path: bool = True           # overall.coa_path (game.py:489-498, facade only)
     tactics: str = "aggressive"     # overall.tactics
     side: str = "blue"              # environment_setup.side
     trained_red: bool = True        # environment_setup.trained_red
@@ -37,6 +38,7 @@ class Scenario:
         hp = cfg.get("hyperparameters", {})
         s = cls(discrete=bool(ov.get("discrete", False)),
                 landing_ops=bool(ov.get("landing_ops", True)),
+                coa_path=bool(ov.get("coa_path", True)),
                 tactics=ov.get("tactics", "aggressive"), side=es.get("side", "blue"),
                 trained_red=bool(es.get("trained_red", True)),
                 red_aggression=float(es.get("red_aggression", 0.4)),

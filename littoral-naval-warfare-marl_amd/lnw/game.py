@@ -11,10 +11,15 @@ Differences from the reference, by design:
     `random` at reset (the reference calls `random` directly); reset-time draws
     (ducting beta(1,3) from numpy's global RNG, landing-ship spawns from
     `random.randint`) use the same global generators as the reference;
-  * observations are float32 values returned in float64 arrays;
-  * analytics side channels (heatmap, coldmap, launch_sites, engagements,
-    blue_ew/red_ew, coa_path) are present but not filled; visualize_* are not
-    provided (out of scope: offline matplotlib).
+  * observations are float32 values returned in float64 arrays; rewards and
+    the cog distance are the float64 values (lnw_set_reward_dtype);
+  * the analytics side channels (engagements, launch_sites, heatmap / coldmap,
+    blue_ew / red_ew, coa_path) are filled from the device logs after every
+    step and get_obs;
+  * visualize_grid / visualize_heatmap (game.py:628-890) draw with matplotlib
+    when it imports (Agg backend without a display) and keep the reference's
+    side effects (imagen counter, engagements cleared, the reset before the
+    heatmap); without matplotlib they only apply those side effects.
 """
 import csv
 import os
@@ -32,6 +37,28 @@ _NAMES = {0: "small", 1: "large", 2: "ls"}
 _DEFAULT_BLUE = {2: [(6, 61), (10, 81)], 3: [(6, 61), (10, 81), (8, 70)],
                  4: [(6, 61), (10, 81), (8, 70), (11, 58)]}   # game.py:551-556
 _LZ = (14, 82)                                                  # game.py:590
+
+
+def _coa_path_on(sc):
+    return getattr(sc, "coa_path", True)
+
+
+def _pyplot():
+    """matplotlib.pyplot with a non-interactive backend when there is no
+    display; None when matplotlib is not installed."""
+    try:
+        import matplotlib
+        if not os.environ.get("DISPLAY"):
+            matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+        return plt
+    except ImportError:
+        return None
+
+
+def _circle(centre, radius):
+    from matplotlib.patches import Circle
+    return Circle(centre, radius, alpha=0.2, edgecolor=None)
 
 
 class ShipSpec:
@@ -209,7 +236,7 @@ class Game:
                 self._g.close()
             self._g = BatchedGame(1, [_NAMES[t] for t in types[:len(blue)]],
                                   [_NAMES[t] for t in types[len(blue):]], scenario=sc,
-                                  device=self.device, grid=grid_arr)
+                                  device=self.device, grid=grid_arr, reward_dtype=torch.float64)
             self._g.enable_analytics(eng_cap=4096, ew_cap=4096, maps=False)
             self._key = key
         g = self._g
@@ -277,8 +304,13 @@ class Game:
         g = self._g
         A = g.A
         rows = [action[a] for a in range(A)]
+        live0 = [s is not None for s in self.blue_ships + self.red_ships]
         if self.scenario.discrete:
-            buf = np.zeros((1, A, 4), np.int32)
+            # an integer ndarray keeps integer semantics (the salvo rewrite of
+            # game.py:379 truncates); list rows (ddqn.py:396) hold Python numbers
+            # and take the rewritten float as is: float64 buffer
+            int_array = isinstance(action, np.ndarray) and action.dtype.kind in "iu"
+            buf = np.zeros((1, A, 4), np.int32 if int_array else np.float64)
             for a, r in enumerate(rows):
                 v = np.asarray(r).reshape(-1)[:4]
                 buf[0, a, :len(v)] = [int(x) for x in v]
@@ -306,7 +338,7 @@ class Game:
             for a in range(g.nb, A):
                 if after[a, 1] != buf[0, a, 1]:
                     try:
-                        rows[a][1] = after[a, 1] if not self.scenario.discrete else int(after[a, 1])
+                        rows[a][1] = after[a, 1].item()
                     except TypeError:
                         pass
         side_blue = self.scenario.side == "blue"
@@ -327,10 +359,102 @@ class Game:
         self.blue_engagements = int(es["blue_engagements"][0])
         self.red_engagements = int(es["red_engagements"][0])
         self.steps_done = int(es["steps_done"][0])
+        if _coa_path_on(self.scenario) and (done == 0 or
+                                           self.steps_done == self.scenario.episode_steps - 1):
+            # game.py:489-498: positions after the step of every ship that was
+            # not None when it began (ships sunk this step included)
+            for a, shp in enumerate(self._all):
+                if live0[a]:
+                    key = "blue" if a < g.nb else ("ls" if shp.ship_type == "ls" else "red")
+                    self.coa_path[key].append(shp.position)
         return obs, [float(r) for r in rew], done, (None if np.isnan(cog) else cog)
 
     def get_grid(self):
         return self.grid
+
+    # ---------------------------------------------------------- visualisation
+    def visualize_grid(self, show=False, path=None, animation=False):
+        """game.py:628-748: terrain, ships, radar circles, replenishment points,
+        EW fixes and engagements of the current state. Side effects kept: the
+        engagement list is cleared and `imagen` counts the frames. The image
+        goes to `path/imagen<k>.png` when a path is given."""
+        plt = _pyplot()
+        if plt is not None:
+            fig, ax = plt.subplots()
+            ax.set_aspect("equal")
+            ax.imshow(np.asarray(self.grid), cmap="gray", origin="upper",
+                      extent=[-0.5, 100 - 0.5, -0.5, 100 - 0.5])
+            marks = {"small": 4, "large": 8, "ls": 6}
+            for col, ships in (("b", self.blue_ships), ("r", self.red_ships)):
+                for shp in ships:
+                    if shp is None:
+                        continue
+                    x, y = shp.position
+                    ax.plot(y, 100 - x - 1, col + ("s" if shp.ship_type == "ls" else "o"),
+                            markersize=marks[shp.ship_type])
+                    if shp.radar_transmission == 1:
+                        r = ((np.sqrt((4 / 3) * 6370 * 2) * (np.sqrt(shp.mast_height / 1000)
+                                                             + np.sqrt(30 / 1000))) / 5
+                             * self.ducting_factor)
+                        ax.add_patch(_circle((y, 100 - x - 1), r))
+            for col, pts in (("bv", self.blue_replenishment_points),
+                             ("rv", self.red_replenishment_points)):
+                for px, py in pts:
+                    ax.plot(py, 100 - px - 1, col, markersize=5)
+            for col, lst in (("b-", self.blue_ew), ("r-", self.red_ew)):
+                for (ox, oy), (fx, fy) in lst:
+                    ax.plot([oy, fy], [100 - ox - 1, 100 - fx - 1], col)
+            for (lx, ly), (tx, ty), msl in self.engagements:
+                ax.plot(ty, 100 - tx - 1, "X", color="orange")
+                ax.plot([ly, ty], [100 - lx - 1, 100 - tx - 1], "-",
+                        color="yellow" if msl == 0 else "orange")
+            ax.set_xlim(-0.5, 100.5)
+            ax.set_ylim(-0.5, 100.5)
+            ax.set_title("Game Grid")
+            if show:
+                plt.show()
+            if path is not None:
+                fig.savefig(os.path.join(path, f"imagen{self.imagen}.png"))
+            plt.close(fig)
+        self.engagements.clear()
+        self.imagen += 1
+
+    def visualize_heatmap(self, heatmap, coldmap, path=None):
+        """game.py:750-890: resets the game (as the reference does first), then
+        draws the terrain with the missile-launch heatmap and the launch-site /
+        end-position cluster centres (KMeans, when scikit-learn imports)."""
+        self.reset(self.num_blue, self.num_red)
+        plt = _pyplot()
+        if plt is None:
+            return
+        fig = plt.figure()
+        plt.imshow(np.asarray(self.grid), cmap="gray", origin="upper",
+                   extent=[-0.5, 100 - 0.5, -0.5, 100 - 0.5])
+        if np.max(heatmap) > 0:
+            plt.imshow(heatmap, cmap="hot", alpha=0.25, origin="upper",
+                       extent=[-0.5, 100 - 0.5, -0.5, 100 - 0.5])
+        try:
+            from sklearn.cluster import KMeans
+        except ImportError:
+            KMeans = None
+        for key in ("blue", "red", "ls"):
+            pts = self.launch_sites.get(key, []) if key != "ls" else []
+            n = self.num_blue if key == "blue" else (self.num_red if key == "red" else 1)
+            if len(pts) < n:
+                pts = self.coa_path[key]
+            if KMeans is None or len(pts) < max(n, 1):
+                continue
+            centres = KMeans(n_clusters=max(n, 1), random_state=0,
+                             n_init="auto").fit(np.asarray(pts)).cluster_centers_
+            for cx, cy in centres:
+                plt.plot(cy, 100 - cx - 1, "yo" if key != "ls" else "rs", markersize=25,
+                         alpha=0.2)
+        if np.max(heatmap) > 0:
+            plt.colorbar()
+        if path is not None:
+            fig.savefig(os.path.join(path, "heatmap.png"))
+        plt.show()
+        plt.close(fig)
 
     def close(self):
         if self._g is not None:

@@ -32,8 +32,9 @@ def replay_gpu(fx, grids, los_mode=0, move_mode=0, contact=False):
     sc = scenario_from_meta(meta, los_mode=los_mode, move_mode=move_mode)
     grid = grids[meta["grid_id"]]
     names = {0: "small", 1: "large", 2: "ls"}
+    # float64 rewards / cog: the reference's Python floats, compared with rtol=0
     g = BatchedGame(E, [names[t] for t in types[:nb]], [names[t] for t in types[nb:]],
-                    scenario=sc, grid=grid)
+                    scenario=sc, grid=grid, reward_dtype=torch.float64)
     g.set_variant(contact)
     # tape slices, one per env
     tapes = [fx["tape"][em["tape_start"]:em["tape_end"]] for em in eps]
@@ -55,7 +56,8 @@ def replay_gpu(fx, grids, los_mode=0, move_mode=0, contact=False):
         if meta["observe"]:
             ob, orr = g.observe(-1)
             yield ("observe", (s, rows), g, (ob.cpu().numpy(), orr.cpu().numpy()))
-        if discrete:
+        list_rows = discrete and meta.get("list_rows", False)
+        if discrete and not list_rows:
             act = np.zeros((E, A, 4), np.int32)
         elif is_f32:
             act = np.zeros((E, A, 4), np.float32)
@@ -67,7 +69,7 @@ def replay_gpu(fx, grids, los_mode=0, move_mode=0, contact=False):
             kinds[e] = fixture_kinds(fx, meta, i)
         at = torch.from_numpy(act).cuda()
         rk = None
-        if not discrete and not is_f32:
+        if (not discrete and not is_f32) or list_rows:
             rk = torch.from_numpy(kinds).cuda()
         out = g.step(at, rk)
         torch.cuda.synchronize()

@@ -271,7 +271,9 @@ def fixture_kinds(fx, meta, step):
     """Per-row value kinds of the recorded actions."""
     A = fx["actions"].shape[1]
     if meta["flags"]["DISCRETE"]:
-        return np.full(A, K_PYINT, np.int32)
+        # list rows (ddqn.py:396): the salvo rewrite stays a float (K_PYFLOAT);
+        # an integer ndarray truncates it (K_PYINT)
+        return np.full(A, K_PYFLOAT if meta.get("list_rows") else K_PYINT, np.int32)
     rf = fx["row_f32"][step]
     if meta["dtype"] == "f32":
         return np.full(A, K_F32, np.int32)

@@ -25,7 +25,8 @@ ep_<name>.npz   full episodes through ``Game.reset`` / ``Game.step``
                 locals with sys.settrace — no reference code is copied), and
                 the per-agent state after every step.
 
-Usage:  python tests/golden/make_golden.py [--quick]
+Usage:  python tests/golden/make_golden.py [--quick] [episodes|los|...]
+        (LNW_GOLDEN_ONLY=ep1,ep2 limits the episode fixtures written)
 """
 import contextlib
 import io
@@ -44,6 +45,8 @@ ASSETS = ["config.json", "red_steps.csv", "red_steps2.csv", "red_steps3.csv",
           "balt_mod_400x400_2.png"]
 
 TYPE_CODE = {"small": 0, "large": 1, "ls": 2, "medium": 3}
+# LNW_GOLDEN_ONLY=name1,name2 regenerates only those episode fixtures
+ONLY_SCENARIOS = [n for n in os.environ.get("LNW_GOLDEN_ONLY", "").split(",") if n]
 
 
 # ----------------------------------------------------------------------------
@@ -362,7 +365,9 @@ def _snapshot(env, ships_all, nb):
 def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_types,
                  spawn="ref", n_ep=4, steps=40, flags=None, dtype="f64",
                  act_lo=0.0, act_hi=1.0, observe=False, grid_id=0, seed=0,
-                 random_ls=0, mixed_rows=False, analytics=False):
+                 random_ls=0, mixed_rows=False, analytics=False, list_rows=False):
+    if ONLY_SCENARIOS and name not in ONLY_SCENARIOS:
+        return
     flags = dict(flags or {})
     F = dict(DISCRETE=False, LANDING_OPS=False, TACTICS="aggressive", SIDE="blue",
              TRAINED_RED=True, RED_AGGRESSION=0.4, N_RED_LANDINGSHIP=random_ls)
@@ -468,7 +473,9 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
                     act = np.stack([rng.integers(0, 2, size=A), rng.integers(0, 5, size=A),
                                     rng.integers(0, 50, size=A)], 1).astype(np.int64)
                     act = np.concatenate([act, np.zeros((A, 1), np.int64)], 1)
-                    call_act = act.copy()
+                    # ddqn.py:396 passes a list of 3-int lists; an ndarray otherwise
+                    call_act = ([[int(v) for v in row[:3]] for row in act] if list_rows
+                                else act.copy())
                     row_f32 = np.zeros(A, np.uint8)
                 else:
                     act = rng.uniform(act_lo, act_hi, size=(A, 4))
@@ -487,7 +494,9 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
                 rec["actions"].append(np.asarray(act, dtype=np.float64))
                 rec["row_f32"].append(row_f32)
                 ret, cap = _capture_step(game, env, call_act)
-                after = np.array([np.asarray(r, dtype=np.float64) for r in call_act])
+                after = np.zeros((A, 4))
+                for a, r in enumerate(call_act):
+                    after[a, :len(r)] = np.asarray(r, dtype=np.float64)
                 rec["actions_after"].append(after)
                 ob = np.zeros((nb, meta["Db"]), np.float32)
                 ob[:, :] = np.asarray(cap["observations"])[0]
@@ -548,7 +557,7 @@ def run_scenario(game, combatant, landingship, name, grids, *, nb_types, nr_type
     tl_cnt, tl_xy = ragged(rec["tl_xy"])
     ptl_cnt, ptl_xy = ragged(rec["pre_tl_xy"])
     meta_all = dict(name=name, flags=F, grid_id=grid_id, dtype=dtype, observe=observe,
-                    episodes=ep_meta, crashes=crashes, mixed_rows=mixed_rows,
+                    episodes=ep_meta, crashes=crashes, mixed_rows=mixed_rows, list_rows=list_rows,
                     landing_zone=(14, 82), episode_steps=steps)
     out = dict(
         meta=np.array(json.dumps(meta_all)),
@@ -619,6 +628,9 @@ def make_episodes(game, combatant, landingship, grids, quick):
                  flags=dict(TRAINED_RED=False))
     run_scenario(game, combatant, landingship, "4v4_discrete", grids, nb_types=S4,
                  nr_types=R4, spawn="melee", n_ep=q(6), seed=11, flags=dict(DISCRETE=True))
+    run_scenario(game, combatant, landingship, "4v4_discrete_lists", grids, nb_types=S4,
+                 nr_types=R4, spawn="melee", n_ep=q(6), seed=18, list_rows=True,
+                 flags=dict(DISCRETE=True, TRAINED_RED=False))
     run_scenario(game, combatant, landingship, "4v4_observe", grids, nb_types=S4,
                  nr_types=R4, spawn="melee", n_ep=q(6), seed=12, observe=True)
     run_scenario(game, combatant, landingship, "4v4_wild", grids, nb_types=S4, nr_types=R4,
