@@ -163,9 +163,11 @@ class BatchedCritic(nn.Module):
         return self.fc4(x)
 
 
-def red_script_table(device="cuda", dtype=torch.float32):
+def red_script_table(device="cuda", dtype=torch.float64):
     """The scripted red profiles (red_steps.csv, red_steps2.csv, red_steps3.csv;
-    game.py:173-182) as a device tensor [3, 40, 4] = [red ship, step, action]."""
+    game.py:173-182) as a device tensor [3, 40, 4] = [red ship, step, action].
+    float64: the reference's CSV rows are Python floats (game.py:181), so a step
+    that contains one runs in float64 (np.asarray upcast, ppo.py:577)."""
     return torch.as_tensor(np.load(os.path.join(DATA, "red_steps.npy")), dtype=dtype, device=device)
 
 
@@ -207,8 +209,10 @@ def discounted_rtg(rewards, gamma):
 
 
 def gae(rewards, values, gamma, lambda_=0.95):
-    """ppo.py:695-714 generalised advantage estimate, batched over leading dims
-    (the sequence runs along the last dim), same operation order."""
+    """ppo.py:695-714 `PPO.gae`, batched over leading dims (the sequence runs
+    along the last dim), same operation order. The reference learner calls it
+    on the reward-to-go and critic values of a minibatch, treating the sampled
+    rows as the sequence (ppo.py:336)."""
     returns = torch.zeros_like(rewards)
     n = rewards.shape[-1]
     g = torch.zeros_like(rewards[..., 0])
@@ -224,69 +228,125 @@ def gae(rewards, values, gamma, lambda_=0.95):
 
 
 class Rollout:
-    """Batched MAPPO rollout (ppo.py:421-671 with the side being trained = blue):
-    every step, the actor acts for all blue ships of all envs from the previous
-    step's observations, red acts from the scripted profiles (untrained red) or
-    a red actor, the step kernel advances all envs, and the critic scores the
-    concatenated blue observations. Buffers are device tensors [E, T, ...].
+    """Batched MAPPO rollout (ppo.py:421-671, side being trained = blue): env e
+    plays one rollout episode; all E envs advance together. Every step t:
 
-    Differences from the reference loop, by design: observations come from the
-    step outputs (plus one `observe` at the start) instead of fresh
-    `ship.get_obs()` calls on the main env (ppo.py:497-500 observes the wrong
-    env); with `stop_at_done` rewards after an env's first `done == 0` are
-    zeroed, as the reference's zero-initialised buffers are after its `break`.
+      1. observe (ppo.py:497-575): `ship.get_obs()` of every live ship, blue
+         then red, with its side effects (target lists, EW gauss draws) — one
+         lnw_observe launch; rows of sunk ships are zeros (compiled_picture);
+      2. the actor acts for every live blue ship (training-mode BatchNorm on a
+         batch-1 call = per-row statistics, bn="sample"); red acts from the
+         scripted profiles (untrained red, ppo.py:563-566) or the red actor in
+         eval mode (ppo.py:569-572, red_bn="running"); sunk ships act
+         np.zeros(4) (ppo.py:515, 574);
+      3. the step runs on what `np.asarray(actions_for_step)` makes of those
+         rows (ppo.py:577): a float32 array when every row is an actor output
+         (all ships alive, red actor-driven), else float64 (a CSV row of Python
+         floats or a np.zeros(4) row upcasts it) — per env, through a float64
+         buffer with per-row value kinds (include/lnw.h);
+      4. the critic scores the concatenated blue observations (ppo.py:598-605).
+
+    Rewards are kept in float64 (the reference's floats). With `stop_at_done`
+    an env's steps after its first done == 0 are masked out (rewards zeroed,
+    `running` False), as the reference `break`s and leaves zeros.
+
+    Differences from the reference loop, by design:
+      * it observes the env it steps; ppo.py:497 calls get_obs on self.env, a
+        Game that rollout() never steps (a reference bug, SURVEY.md §3.3);
+      * exploration: the reference's parameter noise and adaptive noise ratio
+        (ppo.py:466-482, 586-596) belong to the learner; `noise` adds a fixed
+        N(0, noise) term like MLP.forward's `noise` argument;
+      * sunk ships' action rows are stored as zeros (the reference stores the
+        previous ship's `action` variable there, ppo.py:516-517).
+
+    `observe="step"` reuses the step's own output rows instead of a fresh
+    observe (one launch less per step, but not the reference's draw order).
+    `run(forced_actions=...)` replays given actor outputs [E, T, A, 4] instead of
+    sampling (log-probabilities from get_dist): parity against recorded
+    reference rollouts (tests/golden/make_rollout_golden.py).
     """
 
     def __init__(self, game: BatchedGame, actor, critic=None, steps=40, red="script",
-                 red_actor=None, noise=None, bn="sample", gamma=0.99, stop_at_done=True):
+                 red_actor=None, noise=None, bn="sample", red_bn="running", gamma=0.99,
+                 stop_at_done=True, observe="fresh"):
+        if observe not in ("fresh", "step"):
+            raise ValueError("observe must be 'fresh' or 'step'")
         self.g, self.actor, self.critic = game, actor, critic
         self.T, self.red, self.red_actor = int(steps), red, red_actor
-        self.noise, self.bn, self.gamma, self.stop_at_done = noise, bn, float(gamma), stop_at_done
+        self.noise, self.bn, self.red_bn = noise, bn, red_bn
+        self.gamma, self.stop_at_done, self.observe = float(gamma), stop_at_done, observe
         self.table = red_script_table(game.device) if red == "script" else None
 
     @torch.no_grad()
-    def run(self, generator=None):
+    def run(self, generator=None, forced_actions=None):
+        from ._abi import F_ALIVE, LNW_KIND_F32, LNW_KIND_F64
         g = self.g
         E, nb, nr, A, D = g.E, g.nb, g.nr, g.A, g.Db
         dev = g.device
         T = self.T
-        obs = torch.empty((E, T, nb, D), dtype=torch.float32, device=dev)
-        acts = torch.empty((E, T, nb, 4), dtype=torch.float32, device=dev)
-        logp = torch.empty((E, T, nb, 4), dtype=torch.float32, device=dev)
-        rew = torch.zeros((E, T, nb), dtype=torch.float32, device=dev)
+        obs = torch.zeros((E, T, nb, D), dtype=torch.float32, device=dev)
+        acts = torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev)
+        logp = torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev)
+        rew = torch.zeros((E, T, nb), dtype=torch.float64, device=dev)
         val = torch.zeros((E, T), dtype=torch.float32, device=dev)
         running = torch.ones((E, T), dtype=torch.bool, device=dev)
-        full = torch.zeros((E, A, 4), dtype=torch.float32, device=dev)
-        cur = g.observe(-1)[0].clone()
+        f32_step = torch.zeros((E, T), dtype=torch.bool, device=dev)
+        full = torch.zeros((E, A, 4), dtype=torch.float64, device=dev)
+        red_actor_rows = self.red != "script" and self.red_actor is not None
+        if self.observe == "step":
+            g.observe(-1)
         live = torch.ones(E, dtype=torch.bool, device=dev)
         for t in range(T):
+            if self.observe == "fresh":
+                g.observe(-1)
+            cur, cur_red = g.obs_blue, g.obs_red
+            alive = g.get(F_ALIVE).t().bool()  # [E, A], slots not None
+            ab = alive[:, :nb, None]
             obs[:, t] = cur
-            a, lp, _ = self.actor(cur.reshape(E * nb, D), noise=self.noise, bn=self.bn,
-                                  generator=generator)
-            acts[:, t] = a.reshape(E, nb, 4)
-            logp[:, t] = lp.reshape(E, nb, 4)
-            full[:, :nb] = acts[:, t]
+            if forced_actions is not None:
+                a = forced_actions[:, t, :nb].to(torch.float32)
+                lp, _ = self.actor.get_dist(cur.reshape(E * nb, D), a.reshape(E * nb, 4),
+                                            bn=self.bn)
+            else:
+                a, lp, _ = self.actor(cur.reshape(E * nb, D), noise=self.noise, bn=self.bn,
+                                      generator=generator)
+            a = torch.where(ab, a.reshape(E, nb, 4), torch.zeros((), device=dev))
+            acts[:, t] = a
+            logp[:, t] = torch.where(ab, lp.reshape(E, nb, 4), torch.zeros((), device=dev))
+            full[:, :nb] = a
+            ar = alive[:, nb:, None]
             if self.red == "script":
-                full[:, nb:] = red_script_actions(self.table, t, nr)
+                full[:, nb:] = torch.where(ar, red_script_actions(self.table, t, nr),
+                                           torch.zeros((), dtype=torch.float64, device=dev))
             elif self.red_actor is not None:
-                ra, _, _ = self.red_actor(g.obs_red.reshape(E * nr, g.Dr), bn=self.bn,
-                                          generator=generator)
-                full[:, nb:] = ra.reshape(E, nr, 4)
+                if forced_actions is not None:
+                    ra = forced_actions[:, t, nb:].to(torch.float32)
+                else:
+                    ra, _, _ = self.red_actor(cur_red.reshape(E * nr, g.Dr), bn=self.red_bn,
+                                              generator=generator)
+                full[:, nb:] = torch.where(ar, ra.reshape(E, nr, 4),
+                                           torch.zeros((), device=dev)).double()
             else:
                 full[:, nb:] = 0
+            # np.asarray(actions_for_step): float32 only if every row is float32
+            f32 = alive.all(1) if red_actor_rows else torch.zeros(E, dtype=torch.bool, device=dev)
+            f32_step[:, t] = f32
+            kinds = torch.where(f32, LNW_KIND_F32, LNW_KIND_F64).to(torch.uint8)[:, None]
             if self.critic is not None:
                 val[:, t] = self.critic(cur.reshape(E, nb * D)).reshape(E)
-            out = g.step(full)
+            out = g.step(full, kinds.expand(E, A).contiguous())
             running[:, t] = live
-            r = out["rew_blue"]
+            r = out["rew_blue"].to(torch.float64)
             rew[:, t] = torch.where(live[:, None], r, torch.zeros_like(r)) if self.stop_at_done else r
             if self.stop_at_done:
                 live = live & (out["done"] != 0)
-            cur = out["obs_blue"].clone()
         rtg = reference_rtg(rew, self.gamma)
+        # a conventional GAE along each env's time axis over the mean ship
+        # reward; the reference learner instead applies gae() to (reward-to-go,
+        # value) pairs of a sampled minibatch (ppo.py:336), see `gae`
+        gae_time = gae(rew.mean(2), val.double(), self.gamma) if self.critic is not None else None
         return dict(obs=obs, actions=acts, log_probs=logp, rewards=rew, values=val,
-                    running=running, rtg=rtg,
-                    gae=gae(rew.mean(2), val, self.gamma) if self.critic is not None else None)
+                    running=running, f32_step=f32_step, rtg=rtg, gae_time=gae_time)
 
     def capture(self, generator=None):
         """Record one whole rollout (T steps of actor, red, critic, step kernel and

@@ -70,6 +70,7 @@ def test_rollout_buffers():
 def test_rollout_replays_with_stepped_actions():
     """Stepping a second game with the rollout's recorded actions reproduces the
     recorded observations (same seed, scripted red)."""
+    from lnw import _abi
     from lnw.rollout import BatchedActor, Rollout, red_script_actions, red_script_table
     E, T = 128, 8
     g1, g2 = _game(E, seed=9), _game(E, seed=9)
@@ -77,16 +78,17 @@ def test_rollout_replays_with_stepped_actions():
     actor = BatchedActor.for_obs(68).cuda()
     out = Rollout(g1, actor, None, steps=T, stop_at_done=False).run(
         generator=torch.Generator(device="cuda").manual_seed(4))
-    g2.observe(-1)
     tab = red_script_table()
-    full = torch.zeros((E, 8, 4), device="cuda")
+    assert tab.dtype == torch.float64  # CSV rows are Python floats (ppo.py:577 upcast)
+    full = torch.zeros((E, 8, 4), dtype=torch.float64, device="cuda")
     for t in range(T):
+        ob, _ = g2.observe(-1)  # the rollout observes every live ship before acting
+        torch.testing.assert_close(ob, out["obs"][:, t], rtol=0, atol=0)
+        alive = g2.get(_abi.F_ALIVE).t().bool()[:, :, None]
         full[:, :4] = out["actions"][:, t]
-        full[:, 4:] = red_script_actions(tab, t, 4)
+        full[:, 4:] = torch.where(alive[:, 4:], red_script_actions(tab, t, 4), 0.0)
         o = g2.step(full)
-        if t + 1 < T:
-            torch.testing.assert_close(o["obs_blue"], out["obs"][:, t + 1], rtol=0, atol=0)
-        torch.testing.assert_close(o["rew_blue"], out["rewards"][:, t], rtol=0, atol=0)
+        torch.testing.assert_close(o["rew_blue"].double(), out["rewards"][:, t], rtol=0, atol=0)
     g1.close()
     g2.close()
 

@@ -1,0 +1,89 @@
+"""Config 5 pinned to the reference's own MAPPO rollout:
+lnw.rollout.Rollout on the device against fixtures recorded from
+`PPO.rollout` (ppo.py:421-671) by tests/golden/make_rollout_golden.py.
+
+Each recorded rollout episode is one device env, replayed in tape mode (every
+random / gauss / randint / beta draw of the reference), with the reference's
+actor / critic / red-actor weights and its sampled actor outputs replayed
+(`forced_actions`; torch's sampler draws are not the env's). Checked per env
+and step: the observations the actor saw (bit-exact float32), the action
+array's value kind after np.asarray (ppo.py:577), rewards (float64, 1e-5),
+log-probabilities and critic values (float32 network arithmetic on another
+device: 1e-4 / 1e-5), reward-to-go (ppo.py:645-659) and the learner's GAE
+(ppo.py:695-714 on the flattened batch) within 1e-5 relative, and the RNG
+tape consumed draw for draw."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _oracle import GOLDEN, load_fixture
+
+pytestmark = pytest.mark.gpu
+
+NAMES = {0: "small", 1: "large", 2: "ls"}
+
+
+@pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact"])
+def test_rollout_matches_reference(name):
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    from lnw.rollout import BatchedActor, BatchedCritic, Rollout, gae
+    fx = load_fixture(f"rollout_{name}.npz")
+    meta = json.loads(str(fx["meta"]))
+    eps, R, T, nb = meta["episodes"], meta["R"], meta["T"], meta["nb"]
+    types = eps[0]["types"]
+    A = len(types)
+    grid = load_fixture("grids.npz")["grid100"]
+    sc = Scenario(landing_ops=meta["landing_ops"], trained_red=meta["trained_red"],
+                  tactics="aggressive", side="blue", auto_reset=False)
+    g = BatchedGame(R, [NAMES[t] for t in types[:nb]], [NAMES[t] for t in types[nb:]],
+                    scenario=sc, grid=grid, reward_dtype=torch.float64)
+    tapes = [fx["tape"][e["tape_start"]:e["tape_end"]] for e in eps]
+    offs = np.concatenate([[0], np.cumsum([len(t) for t in tapes])]).astype(np.int64)
+    g.set_tape(np.concatenate(tapes), offs)
+    rand_ls = [0] * (A - meta["n_ls"]) + [1] * meta["n_ls"]
+    pos = np.array([e["spawn"] for e in eps], np.int32)
+    g.reset(positions=pos[0], rand_ls=rand_ls, pos_per_env=torch.from_numpy(pos))
+    st = g.agents()
+    assert np.array_equal(np.stack([st["x"], st["y"]], 2), pos), "spawn cells (LS drawn)"
+    assert np.array_equal(g.env_state()["ducting"], [e["ducting"] for e in eps]), "ducting"
+
+    def weights(pre):
+        return {k[len(pre):]: fx[k] for k in fx if k.startswith(pre)}
+
+    actor = BatchedActor.for_obs(g.Db).load_reference(weights("actor.")).cuda()
+    critic = BatchedCritic(g.Db * nb).load_reference(weights("critic.")).cuda()
+    red_actor = None
+    if meta["trained_red"]:
+        red_actor = BatchedActor.for_obs(g.Dr).load_reference(weights("red_actor.")).cuda()
+    r = Rollout(g, actor, critic, steps=T, red="actor" if red_actor is not None else "script",
+                red_actor=red_actor, gamma=meta["gamma"])
+    out = r.run(forced_actions=torch.from_numpy(fx["act"]).cuda())
+    torch.cuda.synchronize()
+    run = out["running"].cpu().numpy()
+    n_steps = np.array(meta["n_steps"])
+    assert np.array_equal(run.sum(1), n_steps)
+    live = run[:, :, None, None]
+    np.testing.assert_array_equal(np.where(live, out["obs"].cpu().numpy(), 0), fx["batch_obs"])
+    np.testing.assert_array_equal(out["f32_step"].cpu().numpy() & run, fx["act_f32"].astype(bool))
+    np.testing.assert_allclose(out["rewards"].cpu().numpy(), fx["rew"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(out["log_probs"].cpu().numpy(), fx["batch_log_probs"], rtol=0,
+                               atol=1e-4)
+    vals = out["values"].cpu().numpy()
+    np.testing.assert_allclose(np.where(run, vals, 0)[:, :, None, None].repeat(nb, 2),
+                               fx["batch_values"], rtol=0, atol=1e-5)
+    rtg = out["rtg"].cpu().numpy()
+    np.testing.assert_allclose(rtg, fx["batch_rtg"][..., 0], rtol=1e-5, atol=1e-5)
+    # the learner's advantage (ppo.py:336) on the flattened batch, values from
+    # the device critic and reward-to-go from the device buffers
+    flat_v = torch.from_numpy(np.where(run, vals, 0)[:, :, None].repeat(nb, 2).reshape(1, -1))
+    adv = gae(out["rtg"].float().cpu().reshape(1, -1), flat_v, meta["gamma"])
+    np.testing.assert_allclose(adv.numpy().reshape(-1), fx["learner_gae"].reshape(-1), rtol=1e-5,
+                               atol=1e-5)
+    # every env consumed exactly its episode's draws
+    used = g.env_state()["rng"]
+    assert np.array_equal(used, [len(t) for t in tapes]), (used, [len(t) for t in tapes])
+    g.close()

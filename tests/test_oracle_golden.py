@@ -192,3 +192,39 @@ def test_episode_tlists_golden(name, grids):
             k = i * A + a
             ref = [tuple(v) for v in xy[offs[k]:offs[k + 1]]]
             assert env.tlist(a) == ref, f"{name} step {i} agent {a}"
+
+
+@pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact"])
+def test_rollout_fixture_env_trajectory(name, grids):
+    """The env side of the recorded reference rollouts (PPO.rollout,
+    make_rollout_golden.py) through the oracle: each step observes every live
+    ship (blue then red, ppo.py:497-575), then steps the recorded action array
+    in its np.asarray kind (ppo.py:577). Observations the actor saw, rewards
+    and the tape consumption must match."""
+    import json
+    fx = load_fixture(f"rollout_{name}.npz")
+    meta = json.loads(str(fx["meta"]))
+    nb, A = meta["nb"], meta["A"]
+    for e, em in enumerate(meta["episodes"]):
+        env = OracleEnv(grids[0], nb, A - nb, landing_ops=meta["landing_ops"],
+                        trained_red=meta["trained_red"])
+        tape = fx["tape"][em["tape_start"]:em["tape_end"]]
+        env.set_tape(tape)
+        rand_ls = [0] * (A - meta["n_ls"]) + [1] * meta["n_ls"]
+        env.reset(np.array(em["types"], np.int32), np.array(em["spawn"], np.int32),
+                  np.array(rand_ls, np.int32))
+        assert env.env_state()["ducting"] == em["ducting"]
+        for t in range(meta["n_steps"][e]):
+            st = env.agents()
+            for a in range(A):
+                if st["alive"][a]:
+                    o = env.observe(a)
+                    if a < nb:
+                        assert np.array_equal(o.astype(np.float32), fx["batch_obs"][e, t, a]), (e, t, a)
+                elif a < nb:
+                    assert not fx["batch_obs"][e, t, a].any()
+            kind = K_F32 if fx["act_f32"][e, t] else K_F64
+            out = env.step(fx["act"][e, t], np.full(A, kind, np.int32))
+            np.testing.assert_allclose(out["rew_blue"], fx["rew"][e, t], rtol=0, atol=1e-12)
+            assert out["done"] == fx["done"][e, t]
+        assert env.env_state()["tape_pos"] == len(tape)

@@ -120,7 +120,15 @@ def test_discounted_rtg():
 def test_red_script_table():
     tab = red_script_table("cpu")
     assert tuple(tab.shape) == (3, 40, 4)
-    assert tab[0, 0].tolist() == [1.0, 0.0, 0.550000011920929, 1.0]
+    # float64: the CSV cells are Python floats (game.py:181), 0.55 stays 0.55
+    assert tab.dtype == torch.float64
+    assert tab[0, 0].tolist() == [1.0, 0.0, 0.55, 1.0]
+    if os.path.isdir("/root/reference"):  # the build container: the CSVs themselves
+        import csv
+        for i, f in enumerate(["red_steps.csv", "red_steps2.csv", "red_steps3.csv"]):
+            with open(os.path.join("/root/reference", f)) as fh:
+                rows = [[float(c) for c in r] for r in csv.reader(fh)]
+            assert tab[i].tolist() == rows[:40]
     a = red_script_actions(tab, 5, 4)
     assert torch.equal(a[:3], tab[:, 5]) and torch.equal(a[3], torch.zeros(4))
     assert torch.equal(red_script_actions(tab, 40, 2), torch.zeros(2, 4))
