@@ -4,13 +4,19 @@
 Driver contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under
 torch.distributed.run, one process per GPU). Prints ONE JSON line on rank 0.
 
-Workload (BASELINE.json metric/configs): 65 536 parallel 4v4 environments per
-GPU on the 100x100 Baltic grid, reference spawns (blue game.py:556; red
-(98,48),(98,52),(98,56),(96,52)), 40-step episodes with in-kernel auto-reset,
-U[0,1)^4 float32 actions from Philox (seed 42), tactics aggressive, side blue,
-trained red. Envs shard across GPUs by global id (weak scaling, no collective
-on the step path). A "step" = one Game.step over every env of the GPU; inputs
+Workload (BASELINE.json metric, config 3): 65 536 parallel 4v4 environments
+on the whole node — rank r of N steps the global envs lnw.shard.env_range
+gives it (65 536 / N each, RNG keyed by global env id), on the 100x100 Baltic
+grid, reference spawns (blue game.py:556; red (98,48),(98,52),(98,56),(96,52)),
+40-step episodes with in-kernel auto-reset, U[0,1)^4 float32 actions from
+Philox (seed 42), tactics aggressive, side blue, trained red. Total work is
+fixed as N grows (strong scaling); `--envs E` instead fixes E envs per GPU
+(weak scaling). A "step" = one Game.step over every env of the GPU; inputs
 (actions for all timed steps) are resident in HBM before the timed region.
+At N=1 the line also carries `secondary` measurements: config 3's per-GPU
+shard (8 192 envs) and config 2 (4 096), melee spawns, the unpruned LOS
+march / A* mode, config 4 and config 5, each with its kernel time and the
+fraction of the HBM roofline its algorithmic bytes reach.
 """
 import argparse
 import ctypes
@@ -64,7 +70,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--envs", type=int, default=65536, help="environments per GPU")
+    p.add_argument("--global-envs", type=int, default=65536,
+                   help="environments over all ranks (BASELINE config 3: 65 536), split by "
+                        "lnw.shard.env_range")
+    p.add_argument("--envs", type=int, default=None,
+                   help="environments per GPU instead (weak scaling)")
     p.add_argument("--spawns", choices=["reference", "melee"], default="reference")
     p.add_argument("--workload", choices=["config3", "config4"], default="config3",
                    help="config3 = the headline 4v4 line; config4 = 8v10+LS on 200x200 "
@@ -75,8 +85,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                    help="threads for the CPU baseline (the GPU box's share is 16 cores)")
-    p.add_argument("--secondary", action="store_true",
-                   help="also time melee spawns and the march/A* variants (stderr + JSON)")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the secondary lines (configs 2, 3-shard, 4, 5, melee, march)")
+    p.add_argument("--secondary-steps", type=int, default=100)
     return p.parse_args()
 
 
@@ -84,14 +95,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_game(E, rank, args, spawns, los_mode, move_mode, cfg=None):
+def make_game(E, env_base, spawns, los_mode, move_mode, cfg=None):
     from lnw.batched import BatchedGame, default_grid
     from lnw.config import Scenario
     if cfg is None:
         sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=True,
                       auto_reset=True, episode_steps=40, los_mode=los_mode, move_mode=move_mode)
         g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc,
-                        device=torch.cuda.current_device(), env_id_base=rank * E, seed=1234)
+                        device=torch.cuda.current_device(), env_id_base=env_base, seed=1234)
         # melee: fleets in contact every step -> the contact variant of the
         # step kernel (lnw_set_variant; identical results)
         g.set_variant(spawns == "melee")
@@ -102,23 +113,34 @@ def make_game(E, rank, args, spawns, los_mode, move_mode, cfg=None):
                   trained_red=True, auto_reset=True, episode_steps=40, los_mode=los_mode,
                   move_mode=move_mode)
     g = BatchedGame(E, cfg["blue"], cfg["red"], scenario=sc, device=torch.cuda.current_device(),
-                    env_id_base=rank * E, seed=1234, grid=default_grid(cfg["G"]))
+                    env_id_base=env_base, seed=1234, grid=default_grid(cfg["G"]))
     n = len(cfg["blue"]) + len(cfg["red"])
     g.reset(positions=[(0, 0)] * n, rand_ls=cfg["rand_ls"], box=cfg["box"])
     return g
 
 
-def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmup, cfg=None):
+def run_workload(E, env_base, spawns, los_mode, move_mode, steps, warmup, cfg=None, digest=False,
+                 count_steps=10):
+    """Create the envs [env_base, env_base + E) of one rank, fill the actions of
+    every step (Philox keyed by global env id and step, so a global env's
+    inputs do not depend on the sharding), run `warmup` untimed steps, then
+    time `steps` launches between barriers. Returns a dict: wall seconds, mean
+    kernel ms from HIP events on the launch stream, envs with error bits,
+    episodes completed, the device work counters (rays / cells marched, A*
+    searches) per env-step over `count_steps` further, untimed steps, and with
+    `digest` the per-env final state."""
     from lnw import _abi
     L = _abi.load()
-    g = make_game(E, rank, args, spawns, los_mode, move_mode, cfg)
+    g = make_game(E, env_base, spawns, los_mode, move_mode, cfg)
     A = g.A
-    # inputs resident before the timed region: actions for every step
+    # inputs resident before the timed region: actions for every step; the
+    # value of (global env, agent, component) at step s sits at Philox counter
+    # offset s * 2^40 + (env * A + agent) * 4 + component
     acts = torch.empty((warmup + steps, E, A, 4), dtype=torch.float32, device="cuda")
     per = E * A * 4
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for s in range(warmup + steps):
-        off = ((rank * (warmup + steps) + s) * per + 3) // 4 * 4
+        off = (s << 40) + env_base * A * 4
         _abi.check(L.lnw_fill_uniform_f32(ctypes.c_void_p(acts[s].data_ptr()), per, 42, off, stream))
     torch.cuda.synchronize()
     for s in range(warmup):
@@ -143,9 +165,47 @@ def run_workload(E, rank, world, args, spawns, los_mode, move_mode, steps, warmu
     st = g.env_state()
     err = int((st["err"] != 0).sum())
     episodes = int(st["episode"].sum())
+    work = None
+    if count_steps > 0 and not digest:
+        # untimed: the same kernels with the work counters bound (atomics)
+        g.count_work(True)
+        for s in range(count_steps):
+            g.step(acts[warmup + s % steps])
+        torch.cuda.synchronize()
+        work = {k: v / (E * count_steps) for k, v in g.work_counts().items()}
+        g.count_work(False)
+    dig = None
+    if digest:
+        ag = g.agents()
+        dig = np.stack([ag["x"], ag["y"], ag["radar"], ag["missiles"], ag["alive"],
+                        ag["steps_done"]], 2).astype(np.int64).reshape(E, -1)
+        dig = np.concatenate([dig, np.stack([st[k] for k in ("n_blue_left", "n_red_left",
+                                                             "steps_done", "episode")], 1),
+                              st["rng"].astype(np.int64)[:, None]], 1)
     g.close()
     del acts
-    return elapsed, kms, err, episodes
+    return dict(elapsed=elapsed, kernel_ms=kms, err=err, episodes=episodes, digest=dig,
+                work_per_env_step=work)
+
+
+def measured_traffic(args, E):
+    """HBM bytes per launch from rocprofv3 PMC counters (2 x FETCH_SIZE +
+    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), as recorded in
+    profiles/traffic.json by tools/gpu/traffic.sh together with the SHA-256 of
+    the liblnw.so it measured. Reported only if this run loads that same
+    library; otherwise null."""
+    import hashlib
+    from lnw import _abi
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        tj = json.load(open(tf))
+        with open(_abi.LIB_PATH, "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()
+        if tj.get("lib_sha256") != sha:
+            return None
+        return tj.get("launch_bytes", {}).get(f"{args.spawns}_e{E}_los{args.los_mode}_mv{args.move_mode}")
+    except (OSError, ValueError):
+        return None
 
 
 def ray_march(n=1 << 22, reps=10):
@@ -274,58 +334,87 @@ def cpu_baseline(seconds, threads):
                 single_thread_value=n1 / dt1)
 
 
+def line_entry(E, res, steps, nb=4, nr=4, desc=""):
+    """One secondary measurement: env-steps/s over the wall clock, the step
+    kernel's mean time and its algorithmic bytes against the HBM roofline,
+    and the device-counted ray-march / A* work per env-step."""
+    B = algorithmic_bytes(nb, nr)
+    el, km = res["elapsed"], res["kernel_ms"]
+    ach = B * E / (km * 1e-3) / 1e9
+    return dict(workload=desc, envs=E, env_steps_per_sec=E * steps / el, ms_per_step=el / steps * 1e3,
+                kernel_ms=km, err_envs=res["err"], work_per_env_step=res["work_per_env_step"],
+                roofline=dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
+                              frac=ach / HBM_PEAK_GBS, algorithmic_bytes_per_env_step=B))
+
+
+def secondary_lines(args):
+    """N=1 only: the other BASELINE configs and kernel modes, each timed like
+    the headline (warmup, then K launches between barriers)."""
+    K, W = args.secondary_steps, min(args.warmup, 20)
+    out = {}
+    for name, E, sp, lm, mm, desc in (
+            ("config3_shard_8192", 8192, "reference", 0, 0,
+             "config 3's per-GPU shard at N=8: 8 192 4v4 envs, reference spawns"),
+            ("config2_4096", 4096, "reference", 0, 0, "config 2: 4 096 4v4 envs, reference spawns"),
+            ("melee_65536", 65536, "melee", 0, 0,
+             "65 536 4v4 envs, melee spawns (contact every step), contact kernel variant"),
+            ("reference_march_astar", 65536, "reference", 1, 1,
+             "65 536 4v4 envs, reference spawns, every LOS query ray-marched, direct A*"),
+            ("reference_los_work", 65536, "reference", 2, 0,
+             "65 536 4v4 envs, reference spawns, plus the reference's LOS work: every own x "
+             "opponent Bresenham ray of every get_obs marched in full (los_mode 2)")):
+        out[name] = line_entry(E, run_workload(E, 0, sp, lm, mm, K, W), K, desc=desc)
+        log(name, out[name])
+    E4 = CONFIG4["envs"]
+    out["config4_8v10ls_g200"] = line_entry(
+        E4, run_workload(E4, 0, "config4", 0, 0, K, W, CONFIG4), K, len(CONFIG4["blue"]),
+        len(CONFIG4["red"]),
+        desc="config 4: 8 192 envs, 8 small blue vs 8 large + 2 landing ships, 200x200, landing ops")
+    log("config4", out["config4_8v10ls_g200"])
+    out["ray_march"] = ray_march()
+    log("ray_march", out["ray_march"])
+    out["config5_mappo_rollout"] = mappo_rollout()
+    log("config5", out["config5_mappo_rollout"])
+    return out
+
+
 def main():
     args = parse()
     from lnw import dist
     world, rank, local = dist.world()
-    torch.cuda.set_device(local)
-    dist.init("nccl")
-    E = args.envs
+    # LNW_FORCE_DEVICE / LNW_DIST_BACKEND: the multi-rank test runs two ranks on
+    # one GPU over gloo (tests/test_gpu_bench_ranks.py); the driver sets neither
+    torch.cuda.set_device(int(os.environ.get("LNW_FORCE_DEVICE", local)))
+    dist.init(os.environ.get("LNW_DIST_BACKEND", "nccl"))
     cfg = CONFIG4 if args.workload == "config4" else None
-    if cfg is not None and E == 65536:
-        E = cfg["envs"]
-    elapsed, kms_mean, err, episodes = run_workload(
-        E, rank, world, args, args.spawns, args.los_mode, args.move_mode, args.steps, args.warmup, cfg)
+    if args.envs is not None:  # weak scaling: E per GPU
+        E, env_base, total = args.envs, rank * args.envs, args.envs * world
+        scaling = "weak"
+    else:
+        total = CONFIG4["envs"] if (cfg is not None and args.global_envs == 65536) else args.global_envs
+        lo, hi = dist.env_range(total, world, rank)
+        E, env_base = hi - lo, lo
+        scaling = "strong"
+    res = run_workload(E, env_base, args.spawns, args.los_mode, args.move_mode, args.steps,
+                       args.warmup, cfg)
+    elapsed, kms_mean, err, episodes = res["elapsed"], res["kernel_ms"], res["err"], res["episodes"]
     elapsed, kms_mean = dist.reduce_max([elapsed, kms_mean])
-    value = world * E * args.steps / elapsed
+    err, episodes = (int(v) for v in dist.reduce_sum([err, episodes]))
+    value = total * args.steps / elapsed
     nb, nr = (len(cfg["blue"]), len(cfg["red"])) if cfg else (4, 4)
     B = algorithmic_bytes(nb, nr)
     achieved = B * E / (kms_mean * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf):
-        try:
-            tj = json.load(open(tf))
-            key = f"{args.spawns}_e{E}_los{args.los_mode}_mv{args.move_mode}"
-            traffic = tj.get(key)
-        except Exception:
-            traffic = None
+    traffic = measured_traffic(args, E)
     secondary = {}
-    if args.secondary and world == 1:
-        for name, sp, lm, mm in (("melee", "melee", 0, 0), ("reference_march_astar", "reference", 1, 1),
-                                 ("melee_march_astar", "melee", 1, 1)):
-            el, km, er, _ = run_workload(E, rank, 1, args, sp, lm, mm, args.steps, args.warmup)
-            secondary[name] = dict(env_steps_per_sec=E * args.steps / el, ms_per_step=km, err_envs=er)
-            log(name, secondary[name])
-        E4 = CONFIG4["envs"]
-        el, km, er, _ = run_workload(E4, rank, 1, args, "config4", 0, 0, args.steps, args.warmup,
-                                     CONFIG4)
-        B4 = algorithmic_bytes(len(CONFIG4["blue"]), len(CONFIG4["red"]))
-        secondary["config4_8v10ls_g200"] = dict(
-            env_steps_per_sec=E4 * args.steps / el, ms_per_step=km, err_envs=er, envs=E4,
-            algorithmic_bytes_per_env_step=B4, achieved_GBs=B4 * E4 / (km * 1e-3) / 1e9)
-        log("config4", secondary["config4_8v10ls_g200"])
-        secondary["ray_march"] = ray_march()
-        log("ray_march", secondary["ray_march"])
-        secondary["config5_mappo_rollout"] = mappo_rollout()
-        log("config5", secondary["config5_mappo_rollout"])
+    if world == 1 and not args.no_secondary and cfg is None:
+        secondary = secondary_lines(args)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
     if rank == 0:
         line = {
-            "metric": "env-steps/sec (whole node), 65536 parallel 4v4 envs on 100x100 grid"
-                      if cfg is None else "env-steps/sec, config 4 (diagnostic line)",
+            "metric": (f"env-steps/sec (whole node), {total} parallel 4v4 envs on 100x100 grid"
+                       if cfg is None else f"env-steps/sec, config 4 ({total} envs, diagnostic line)"),
             "value": value,
             "unit": "env-steps/sec",
             "n_gpus": world,
@@ -333,18 +422,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64+i32",
             "data": "synthetic",
             "config": {
-                "workload": (f"{E} parallel 4v4 envs per GPU, 100x100 Baltic grid, "
-                             f"{args.spawns} spawns, 40-step episodes with auto-reset, "
-                             "U[0,1)^4 f32 actions") if cfg is None else
-                            (f"{E} parallel 8v8+2LS envs per GPU (config 4), 200x200 grid, "
-                             "box spawns, landing ops, 40-step episodes with auto-reset, "
-                             "U[0,1)^4 f32 actions"),
-                "envs_per_gpu": E, "global_envs": world * E,
+                "workload": (f"{total} parallel 4v4 envs over {world} GPU(s) ({E} on rank 0), "
+                             f"100x100 Baltic grid, {args.spawns} spawns, 40-step episodes with "
+                             "auto-reset, U[0,1)^4 f32 actions") if cfg is None else
+                            (f"{total} parallel 8v8+2LS envs (config 4) over {world} GPU(s), "
+                             "200x200 grid, box spawns, landing ops, 40-step episodes with "
+                             "auto-reset, U[0,1)^4 f32 actions"),
+                "global_envs": total, "envs_per_gpu": E,
                 "agents": "4v4" if cfg is None else f"{nb}v{nr}",
                 "grid": 100 if cfg is None else cfg["G"],
                 "spawns": args.spawns if cfg is None else "box",
@@ -366,12 +455,15 @@ def main():
         if cfg is None and args.spawns == "reference" and args.los_mode == 0:
             # SURVEY §8(d) secondary work metric: the reference marches a Bresenham
             # ray for every own x opponent pair of every get_obs, 10 996 cells per
-            # 4v4 env-step at these spawns (measured there); the build answers every
-            # LOS query it needs from the LOS table and at these spawns needs none
-            # (no pair inside a sensor range), so it marches 0 cells
+            # 4v4 env-step at these spawns (measured there)
+            w = res["work_per_env_step"] or {}
             line["los_work"] = {"reference_equivalent_cells_per_env_step": REF_LOS_CELLS,
                                 "reference_equivalent_cells_per_sec": REF_LOS_CELLS * value,
-                                "marched_cells_per_env_step": 0}
+                                "marched_cells_per_env_step": w.get("cells_marched"),
+                                "marched_rays_per_env_step": w.get("rays_marched"),
+                                "astar_searches_per_env_step": w.get("astar_searches"),
+                                "counted_over": "10 untimed steps after the timed region, "
+                                                "rank 0, device counters (lnw_set_counters)"}
         if secondary:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)

@@ -107,7 +107,10 @@ typedef struct lnw_params {
     /* build-side knobs (not in the reference) */
     int32_t episode_steps;   /* auto-reset horizon (0 = never)          */
     int32_t auto_reset;      /* reset an env in-kernel when done==0 or at the horizon */
-    int32_t los_mode;        /* 0 = precomputed LOS table, 1 = ray march   */
+    int32_t los_mode;        /* 0 = precomputed LOS table, 1 = ray march,
+                                2 = table + the reference's LOS work: every
+                                own x opponent ray marched in full at each
+                                get_obs and discarded (diagnostics)        */
     int32_t move_mode;       /* 0 = precomputed move table, 1 = direct A*  */
 } lnw_params;
 
@@ -199,6 +202,15 @@ int lnw_set_epw(lnw_handle *h, int32_t epw);
  * faster when fleets are in contact every step (melee, MAPPO rollouts against
  * a closing red) but slower on the quiet path, which shares the kernel. */
 int lnw_set_variant(lnw_handle *h, int32_t contact);
+
+/* Work counters (diagnostics, no reference counterpart): while bound, the step
+ * and observe kernels add to counters_dev[0] the LOS rays they ray-march
+ * (queries outside the LOS table, or every query with los_mode = 1), to [1] the
+ * Bresenham cells those rays visit (combatant.py:411-456) and to [2] the A*
+ * searches they run (targets outside the move table, or move_mode = 1;
+ * combatant.py:289-408). counters_dev: [4] uint64 device array, or NULL to
+ * unbind. Costs one uniform branch per march / search while unbound. */
+int lnw_set_counters(lnw_handle *h, uint64_t *counters_dev);
 
 /* Reward / cog output type of lnw_step. f64 = 0 (default): rew_blue, rew_red and
  * cog are float32 arrays; f64 = 1: they are float64 arrays (pass double* cast to

@@ -77,6 +77,7 @@ struct KState {
   float *dummy;            // [WAVE * 4] sink for masked-out stores (keeps store counts static)
   unsigned long long *prof;  // diagnostics (LNW_PROF): [n_wg][16] phase timestamps, else null
   lnw_analytics ana;         // analytics side channels (null pointers: off)
+  unsigned long long *ctr;   // lnw_set_counters work counters (null: off)
   const uint32_t *mask2;   // [G][W16] 2 bits per cell: bit0 > move_thr, bit1 > ew_thr
   const uint32_t *mvtab;   // [2][G*G][3]
   const uint32_t *lostab;  // [G*G][486]
@@ -300,15 +301,17 @@ __device__ inline uint32_t cell_bits(const uint32_t *mask2, int W16, int x, int 
 // bit0 = radar clear (no cell > move_thr), bit1 = EW clear (no cell > ew_thr).
 // With early_exit, stops at the first radar-blocked cell (EW is only ever
 // consulted after radar LOS passed, combatant.py:110,119).
+// ncell (optional): incremented by the number of cells visited.
 template <bool early_exit>
 __device__ inline uint32_t los_march(const uint32_t *mask2, int W16, int x1, int y1, int x2,
-                                     int y2) {
+                                     int y2, int *ncell = nullptr) {
   int dx = abs(x2 - x1), dy = abs(y2 - y1);
   int sx = x1 > x2 ? -1 : 1, sy = y1 > y2 ? -1 : 1;
   int err = dx - dy;
   uint32_t blk = 0;
   for (;;) {
     blk |= cell_bits(mask2, W16, x1, y1);
+    if (ncell) ++*ncell;
     if (early_exit && (blk & 1u)) return 0u;
     if (x1 == x2 && y1 == y2) break;
     int e2 = 2 * err;

@@ -265,6 +265,7 @@ __device__ inline bool check_path_h(const KParams &P, const KState &S, int type,
   }
   MaskBlocked mb{S.mask2, P.W16};
   bool sb = mb(sx, sy);
+  if (S.ctr) atomicAdd(&S.ctr[2], 1ull);  // A* searches run (work counter)
   return check_path_dev(mb, sb, P.G, type, sx, sy, tx, ty, open, ost);
 }
 
@@ -273,17 +274,30 @@ __device__ inline bool can_move_to_h(const KParams &P, const KState &S, int x, i
   return false;
 }
 
+// Bresenham ray march of the step / observe kernels, counted into the work
+// counters when they are bound (lnw_set_counters: [0] rays marched, [1] cells
+// visited)
+__device__ inline uint32_t los_march_c(const KState &S, const uint32_t *mask, int W16, int x1,
+                                       int y1, int x2, int y2) {
+  if (!S.ctr) return los_march<true>(mask, W16, x1, y1, x2, y2);
+  int n = 0;
+  const uint32_t r = los_march<true>(mask, W16, x1, y1, x2, y2, &n);
+  atomicAdd(&S.ctr[0], 1ull);
+  atomicAdd(&S.ctr[1], (unsigned long long)n);
+  return r;
+}
+
 // LOS query: table lookup inside the +-40 window, otherwise the ray march
 __device__ inline uint32_t los_q(const KParams &P, const KState &S, const uint32_t *mask, int x1,
                                  int y1, int x2, int y2) {
   int dx = x2 - x1, dy = y2 - y1;
-  if (P.los_mode == 0 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS) {
+  if (P.los_mode != 1 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS) {
     int col = (dy + R_LOS) * 2;
     uint32_t w = S.lostab[((size_t)x1 * P.G + y1) * LOS_CELL_WORDS + (dx + R_LOS) * LOS_ROW_WORDS +
                           (col >> 5)];
     return (w >> (col & 31)) & 3u;
   }
-  return los_march<true>(mask, P.W16, x1, y1, x2, y2);
+  return los_march_c(S, mask, P.W16, x1, y1, x2, y2);
 }
 
 // ---------------------------------------------------------------------------
@@ -608,6 +622,36 @@ __device__ __forceinline__ T rsel(const T (&a)[N], int k) {
 // get_obs sensor fusion (combatant.py:90-161 / landingship.py:94-165) for
 // runtime ship counts: refreshes agent me's target list (observation floats are
 // written in phase O).
+// los_mode 2 (reference work, diagnostics): the reference traces the full
+// Bresenham line of every own ship x opponent pair at every get_obs before
+// testing any range (combatant.py:106-110, 443-454). March those rays in full
+// (no early exit, counted by lnw_set_counters) and discard them; the step's
+// own LOS answers still come from the table, so results do not change.
+__device__ __forceinline__ void march_pairs_ref(Ctx &X, int me) {
+  const KParams &P = X.P;
+  const Cols &c = X.c;
+  const int lane = X.lane;
+  const int side = me >= P.nb;
+  const int own0 = side ? P.nb : 0, own1 = side ? P.A : P.nb;
+  const int opp0 = side ? 0 : P.nb, opp1 = side ? P.nb : P.A;
+  uint32_t acc = 0;
+  for (int i = own0; i < own1; i++) {
+    if (!COLB(c.alive0, i)) continue;
+    const uint32_t pi = COLW(c.pos_cur, i);
+    for (int j = opp0; j < opp1; j++) {
+      if (!COLB(c.alive0, j)) continue;
+      const uint32_t pj = COLW(c.pos_cur, j);
+      int n = 0;
+      acc += los_march<false>(X.S.mask2, P.W16, pos_x(pi), pos_y(pi), pos_x(pj), pos_y(pj), &n);
+      if (X.S.ctr) {
+        atomicAdd(&X.S.ctr[0], 1ull);
+        atomicAdd(&X.S.ctr[1], (unsigned long long)n);
+      }
+    }
+  }
+  if (acc == 0xffffffffu) X.S.dummy[lane] = 0.0f;  // keeps the marches (never true)
+}
+
 __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
   const KParams &P = X.P;
   const KState &S = X.S;
@@ -682,7 +726,7 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
       radm |= (rad_ok ? 1u : 0u) << u;
       closem |= (close ? 1u : 0u) << u;
       ewm |= (ew_cand ? 1u : 0u) << u;
-      if (P.los_mode == 0 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS) {
+      if (P.los_mode != 1 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS) {
         tabm |= 1u << u;
         wi[u] = ((uint32_t)(pos_x(pi) * P.G + pos_y(pi)) * LOS_CELL_WORDS + (dx + R_LOS) * LOS_ROW_WORDS) *
                     32u + (dy + R_LOS) * 2;
@@ -1168,7 +1212,7 @@ __device__ inline void los_prefetch_t(Ctx &X) {
       bool need;
       ray(r0 + u, x1, y1, x2, y2, need);
       const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR);
-      bits[s] |= (uint64_t)los_march<true>(X.mask, P.W16, x1, y1, x2, y2) << (2 * q);
+      bits[s] |= (uint64_t)los_march_c(X.S, X.mask, P.W16, x1, y1, x2, y2) << (2 * q);
     }
   }
   X.lpre[0] = bits[0];
@@ -2190,7 +2234,10 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // observation copy-out); NB = NR = 0: runtime counts from P.
 // NB/NR > 0 run two waves per workgroup: wave 0 steps the envs, wave 1 emits
 // the observation rows (emit_wave_t).
-template <int NB, int NR, bool CW = false>
+// REFW: los_mode 2's reference LOS work (march_pairs_ref), a separate
+// instantiation of the runtime-size kernel so the production kernels carry none
+// of its code
+template <int NB, int NR, bool CW = false, bool REFW = false>
 __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
@@ -2213,7 +2260,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
-  const bool emit = ST && P.los_mode == 0 && nenv == WAVE && !(P.dbg_skip & 3);
+  const bool emit = ST && P.los_mode != 1 && nenv == WAVE && !(P.dbg_skip & 3);
   // two-wave workgroups share phases L and M (agents / pair passes split);
   // after M wave 1 turns to emission and wave 0 runs S
   constexpr int NW = ST && EPW == WAVE ? 2 : 1;
@@ -2249,7 +2296,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   const bool astar = NW > 1 ? __syncthreads_or(pend) != 0 : true;
   // quiet workgroups (lnw_quiet.inc) skip phase S; deciding it needs the final
   // moves, so wave 0 runs the A* fallback before a second barrier
-  const bool qcap = emit && !(P.dbg_skip & 512);
+  // (any workgroup size: a partial or small-epw workgroup idles its extra lanes)
+  const bool qcap = ST && P.los_mode == 0 && !(P.dbg_skip & 3) && !(P.dbg_skip & 512);
   if constexpr (ST && NW > 1) {
     if (qcap) {
       if (wid == 0) prof_stamp(S, 6);
@@ -2262,7 +2310,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       if (wid == 0) prof_stamp(S, 8);
       if (wq) {
         quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
-                             rew_r, done_out, cog_out, env0);
+                             rew_r, done_out, cog_out, env0, nenv, valid);
         return;
       }
     }
@@ -2288,7 +2336,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
           r2col[lane], 0};
     unsigned long long tp[4] = {0, 0, 0, 0}, t0 = prof_now(S);  // LNW_PROF part totals
     if constexpr (ST) {
-      if (P.los_mode == 0 && !(P.dbg_skip & 2048)) los_prefetch_t<NB, NR>(X);
+      if (P.los_mode != 1 && !(P.dbg_skip & 2048)) los_prefetch_t<NB, NR>(X);
     }
     tp[1] += prof_now(S) - t0;
     Neut N{{0, 0}, {0u, 0u}};
@@ -2359,6 +2407,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       tp[0] += prof_now(S) - t0;
       t0 = prof_now(S);
       if (al && !(P.dbg_skip & 128)) {
+        if constexpr (REFW) march_pairs_ref(X, a);
         if constexpr (ST) {
           if (!side) get_obs_t<NB, NR, CW>(X, a, 0, NB);
           else get_obs_t<NR, NB, CW>(X, a, NB, 0);
@@ -2427,6 +2476,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
     else if (sel == LNW_OBS_RED) { a0 = nb; }
     for (int a = a0; a < a1; a++) {
       if (!COLB(c.alive0, a)) continue;
+      if (P.los_mode == 2) march_pairs_ref(X, a);
       get_obs_dev(X, a);
       COLB(c.obsd, a) = 1;
       S.tl_cnt[(size_t)a * E + env] = (uint16_t)COLW(c.tcnt, a);
@@ -2659,6 +2709,7 @@ struct lnw_handle {
   float *d_gridf = nullptr, *d_winf = nullptr, *d_dummy = nullptr;
   unsigned long long *d_prof = nullptr;  // LNW_PROF phase timestamps
   lnw_analytics ana{};                   // bound analytics buffers (lnw_set_analytics)
+  unsigned long long *ctr = nullptr;     // bound work counters (lnw_set_counters)
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
   bool prof = false, force_generic = false;
@@ -2698,7 +2749,7 @@ KState make_state(lnw_handle *h) {
   s.type = h->type; s.steps = h->steps; s.dist_lz = h->dist_lz; s.tl_cnt = h->tl_cnt; s.tl = h->tl;
   s.duct = h->duct; s.envi = h->envi; s.rng = h->rng; s.err = h->err;
   s.bear_val = h->bear_val; s.bear_ship = h->bear_ship; s.atan_deg = h->d_atan;
-  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.ana = h->ana; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
+  s.grid = h->d_grid; s.gridf = h->d_gridf; s.winf = h->d_winf; s.dummy = h->d_dummy; s.prof = nullptr; s.ana = h->ana; s.ctr = h->ctr; s.mask2 = h->d_mask2; s.mvtab = h->d_mvtab; s.lostab = h->d_lostab;
   s.tape = h->tape; s.tape_off = h->tape_off;
   s.sp_types = h->sp_types; s.sp_pos = h->sp_pos; s.sp_randls = h->sp_randls;
   s.sp_pos_env = h->sp_pos_env_on ? h->sp_pos_env : nullptr;
@@ -2712,8 +2763,8 @@ size_t step_lds_bytes(const lnw_handle *h) {
 }
 
 // Environments per workgroup: EPW (one env per lane) unless that leaves the GPU
-// with fewer workgroups than it can hold at once; then halve it (down to 1) until
-// the grid fills every resident slot. A step is a per-lane latency chain, so a
+// with fewer workgroups than it can hold at once; then halve it (down to 16 for
+// the two-wave kernels, 1 otherwise) until the grid fills every resident slot. A step is a per-lane latency chain, so a
 // workgroup with fewer live lanes takes about as long as a full one, and more
 // workgroups in flight finish the batch in fewer rounds (config 4: 8 192 envs
 // -> 512 workgroups of 16 instead of 128 of 64). LNW_EPW_RT overrides.
@@ -2726,15 +2777,19 @@ int choose_epw(const lnw_handle *h) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
     ncu = prop.multiProcessorCount;
-  const bool two_wave = !h->force_generic && h->nb == h->nr && h->nb >= 2 && h->nb <= 4 && EPW == WAVE;
+  const bool two_wave = !h->force_generic && h->params.los_mode != 2 && h->nb == h->nr && h->nb >= 2 && h->nb <= 4 && EPW == WAVE;
   const size_t lds = step_lds_bytes(h) + 1024;
   int per_cu = (int)((160 * 1024) / lds);
   const int by_waves = two_wave ? 4 : 8;  // 256 VGPRs: two waves per SIMD
   if (per_cu > by_waves) per_cu = by_waves;
   if (per_cu < 1) per_cu = 1;
   const long long slots = (long long)ncu * per_cu;
+  // two-wave kernels stop at 16 envs per workgroup: below that each workgroup's
+  // fixed head (terrain mask staging, state columns) outweighs the shorter
+  // chain (8 192 envs: 20.2 us at 16, 20.5 at 8, 22.3 at 32, 29.0 at 64)
+  const int min_epw = two_wave ? 16 : 1;
   int epw = EPW;
-  while (epw > 1 && (h->E + epw - 1) / epw < slots) epw /= 2;
+  while (epw > min_epw && (h->E + epw - 1) / epw < slots) epw /= 2;
   if ((h->E + epw - 1) / epw > slots && epw < EPW) epw *= 2;  // never more rounds than EPW needs
   return epw;
 }
@@ -2964,10 +3019,11 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     size_t need = step_lds_bytes(h) + 1024;
     if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     if (need > 64 * 1024) {
-      const void *ks[8] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
+      const void *ks[9] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
                            (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
                            (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
-                           (const void *)step_kernel<4, 4, true>, (const void *)observe_kernel};
+                           (const void *)step_kernel<4, 4, true>, (const void *)step_kernel<0, 0, false, true>,
+                           (const void *)observe_kernel};
       for (const void *kk : ks)
         HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
     }
@@ -3050,15 +3106,16 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
     s.prof = h->d_prof;
   }
   bool generic = h->force_generic;
-#define LNW_STEP(NB_, NR_, CW_)                                                                  \
-  step_kernel<NB_, NR_, CW_><<<grid, dim3(NB_ > 0 && EPW == WAVE ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
+#define LNW_STEP(NB_, NR_, CW_, RW_)                                                             \
+  step_kernel<NB_, NR_, CW_, RW_><<<grid, dim3(NB_ > 0 && EPW == WAVE ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
                                                  done_dev, cog_dev)
   const bool cw = h->contact;
-  if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true); else LNW_STEP(4, 4, false); }
-  else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true); else LNW_STEP(3, 3, false); }
-  else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true); else LNW_STEP(2, 2, false); }
-  else LNW_STEP(0, 0, false);
+  if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
+  else if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
+  else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
+  else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
+  else LNW_STEP(0, 0, false, false);
 #undef LNW_STEP
   HIPCHK(hipGetLastError());
   if (s.prof) prof_report(h, st, (int)grid.x);
@@ -3101,6 +3158,12 @@ int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbyte
 }
 
 int lnw_tlist_cap(lnw_handle *h) { return h ? h->T : LNW_EINVAL; }
+
+int lnw_set_counters(lnw_handle *h, uint64_t *counters_dev) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  h->ctr = (unsigned long long *)counters_dev;
+  return 0;
+}
 
 int lnw_set_reward_dtype(lnw_handle *h, int32_t f64) {
   if (!h) return fail(LNW_EINVAL, "null handle");

@@ -25,6 +25,7 @@ SYMBOLS = [
     "lnw_abi_version", "lnw_last_error", "lnw_create", "lnw_destroy", "lnw_load_terrain",
     "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_state_field", "lnw_tlist_cap",
     "lnw_set_epw", "lnw_set_variant", "lnw_set_reward_dtype",
+    "lnw_set_counters",
     "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
     "lnw_fill_uniform_f32", "lnw_hit_tables", "lnw_set_analytics", "lnw_actor_features",
 ]
@@ -83,6 +84,7 @@ def load(path=None):
         "lnw_set_epw": ([P, I32], C.c_int),
         "lnw_set_variant": ([P, I32], C.c_int),
         "lnw_set_reward_dtype": ([P, I32], C.c_int),
+        "lnw_set_counters": ([P, P], C.c_int),
         "lnw_los_batch": ([P, I32, P, I64, I32, I32, P, P], C.c_int),
         "lnw_astar_batch": ([P, I32, I32, P, P, P, I64, P, P, P, P], C.c_int),
         "lnw_move_batch": ([P, P, P, P, P, I64, P, P, P], C.c_int),

@@ -249,6 +249,19 @@ class BatchedGame:
         return dict(heatmap=t["heatmap"], coldmap=t["coldmap"], launch=t["launch"],
                     engagements=eng, engagements_total=n_eng, ew_fixes=ew, ew_total=n_ew)
 
+    def count_work(self, on=True):
+        """Bind (on) or unbind the device work counters (lnw_set_counters):
+        rays ray-marched, Bresenham cells visited, A* searches run."""
+        if on:
+            self._ctr = torch.zeros(4, dtype=torch.int64, device=self.device)
+            check(self.L.lnw_set_counters(self.h, _ptr(self._ctr)))
+        else:
+            check(self.L.lnw_set_counters(self.h, None))
+
+    def work_counts(self):
+        c = self._ctr.cpu().tolist()
+        return dict(rays_marched=c[0], cells_marched=c[1], astar_searches=c[2])
+
     def observe(self, agent=-1):
         """ship.get_obs() for every live ship (agent=-1, blue then red), one side
         (-2 blue, -3 red) or one agent index, in every env."""

@@ -26,7 +26,7 @@ class Scenario:
     landing_zone: tuple = (14, 82)  # game.py:590
     # build-side knobs
     auto_reset: bool = False
-    los_mode: int = 0               # 0 LOS table, 1 ray march
+    los_mode: int = 0               # 0 LOS table, 1 ray march, 2 table + reference LOS work
     move_mode: int = 0              # 0 move table, 1 direct A*
 
     @classmethod

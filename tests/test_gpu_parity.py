@@ -522,26 +522,32 @@ def test_quiet_path_vs_oracle(grids, trained_red):
     g.close()
 
 
-@pytest.mark.parametrize("trained_red", [True, False])
+@pytest.mark.parametrize("E,trained_red", [(256, True), (256, False), (8192, True), (4133, False)])
 @pytest.mark.parametrize("spawns", ["reference", "mixed"])
-def test_quiet_path_vs_phase_s_long(grids, spawns, trained_red):
+def test_quiet_path_vs_phase_s_long(grids, spawns, trained_red, E, monkeypatch):
     """The bench workload shape (auto-reset, 40-step episodes, Philox) over 90
-    steps: 64 envs per workgroup (quiet path where it applies) against 16 per
-    workgroup (phase S + phase O everywhere): identical observations, rewards,
-    done, cog and final state. "mixed": workgroups 1 and 3 spawn (and re-spawn)
-    in the melee box, 0 and 2 at the reference spawns."""
+    steps, three launch shapes with identical results (observations, rewards,
+    done, cog, written-back actions, final state): 64 envs per workgroup (quiet
+    path where it applies), 8 envs per workgroup (the quiet path in partial
+    two-wave workgroups, the small-E launch shape), and 64 per workgroup with
+    the quiet path disabled (LNW_DEBUG_SKIP bit 9: phase S everywhere). E = 8 192
+    is config 3's per-GPU shard; 4 133 leaves a ragged last workgroup. "mixed":
+    every second group of 64 envs spawns (and re-spawns) in the melee box."""
     from lnw import _abi
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
     sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40, trained_red=trained_red)
-    E = 256
     pos = np.array([REF_SPAWNS] * E, np.int32)
     if spawns == "mixed":
-        for w in (1, 3):
-            pos[64 * w:64 * (w + 1)] = _melee_positions(grids[0], 64, 4, 4, seed=w)
+        for w in range(1, (E + 63) // 64, 2):
+            n = min(64, E - 64 * w)
+            pos[64 * w:64 * w + n] = _melee_positions(grids[0], n, 4, 4, seed=w)
     games = []
-    for epw in (64, 16):
+    for epw, skip in ((64, None), (8, None), (64, "512")):
+        if skip:
+            monkeypatch.setenv("LNW_DEBUG_SKIP", skip)  # read once, by lnw_create
         g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=9)
+        monkeypatch.delenv("LNW_DEBUG_SKIP", raising=False)
         assert g.set_epw(epw) == epw
         g.reset(positions=REF_SPAWNS, pos_per_env=torch.from_numpy(pos))
         games.append(g)
@@ -550,15 +556,19 @@ def test_quiet_path_vs_phase_s_long(grids, spawns, trained_red):
         act = torch.from_numpy(rng.random((E, 8, 4)).astype(np.float32)).cuda()
         acts = [act.clone() for _ in games]
         outs = [{k: v.cpu().numpy().copy() for k, v in g.step(a).items()} for g, a in zip(games, acts)]
-        for k in outs[0]:
-            assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), (s, k)
-        assert torch.equal(acts[0], acts[1]), (s, "actions written back")
+        for o in outs[1:]:
+            for k in outs[0]:
+                assert np.array_equal(outs[0][k], o[k], equal_nan=True), (s, k)
+        for a in acts[1:]:
+            assert torch.equal(acts[0], a), (s, "actions written back")
     sts = [g.env_state() for g in games]
-    for k in sts[0]:
-        assert np.array_equal(sts[0][k], sts[1][k], equal_nan=True), k
+    for st in sts[1:]:
+        for k in sts[0]:
+            assert np.array_equal(sts[0][k], st[k], equal_nan=True), k
     for f in range(_abi.F_TL):  # per-agent fields (target-list contents: via counts)
-        a, b = (g.get(f).cpu().numpy() for g in games)
-        assert np.array_equal(a, b, equal_nan=True), f
+        a = games[0].get(f).cpu().numpy()
+        for g in games[1:]:
+            assert np.array_equal(a, g.get(f).cpu().numpy(), equal_nan=True), f
     for g in games:
         g.close()
 
@@ -666,3 +676,44 @@ def test_quiet_path_dtypes_vs_oracle(grids, mode, trained_red):
             assert np.allclose(rr[e], r["rew_red"], rtol=0, atol=REW_TOL), (s, e, "rew_red")
             assert dn[e] == r["done"], (s, e, "done")
     g.close()
+
+
+def test_work_counters(grids):
+    """lnw_set_counters: the table path at the reference spawns marches no ray
+    and runs no A*; the unpruned mode (los_mode 1, move_mode 1) marches every
+    pair get_obs tests and runs an A* per live ship per step; results do not
+    change with the counters bound."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    E = 256
+    counts = {}
+    for mode in (0, 1, 2):
+        sc = Scenario(landing_ops=False, auto_reset=True, los_mode=mode, move_mode=mode % 2)
+        g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=3)
+        g.reset(positions=REF_SPAWNS)
+        rng = np.random.default_rng(1)
+        acts = [torch.from_numpy(rng.random((E, 8, 4)).astype(np.float32)).cuda() for _ in range(6)]
+        ref = [{k: v.clone() for k, v in g.step(a.clone()).items()} for a in acts[:3]]
+        g.set_rng(3)  # the same draws again (the reset draws the ducting)
+        g.reset(positions=REF_SPAWNS)
+        g.count_work(True)
+        for a, r in zip(acts[:3], ref):
+            out = g.step(a.clone())
+            for k in r:
+                assert torch.equal(out[k], r[k]) or torch.allclose(out[k], r[k], equal_nan=True), k
+        torch.cuda.synchronize()
+        counts[mode] = g.work_counts()
+        g.count_work(False)
+        g.close()
+    assert counts[0] == dict(rays_marched=0, cells_marched=0, astar_searches=0), counts[0]
+    c = counts[1]
+    # at most one A* per live ship per step (8 ships x 3 steps x E); at these
+    # spawns the march mode's range pruning leaves no pair to march
+    assert 0 < c["astar_searches"] <= 8 * 3 * E, c
+    assert c["rays_marched"] == c["cells_marched"] == 0, c
+    # los_mode 2 (the reference's LOS work): 8 get_obs x 4 x 4 pairs per env-step,
+    # every ray in full; the reference measured 85.9 cells per ray at these spawns
+    # (SURVEY.md §8(a) a8)
+    c = counts[2]
+    assert c["rays_marched"] == 128 * 3 * E and c["astar_searches"] == 0, c
+    assert 70 < c["cells_marched"] / c["rays_marched"] < 100, c

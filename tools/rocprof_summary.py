@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 runs of tools/gpu/prof_r01.sh into profiles/<tag>_*.
+"""Summarise the rocprofv3 runs of tools/gpu/prof.sh into profiles/<tag>_*.
 
-Reads gpurun_out/prof_kt (kernel trace + stats) and the separate --pmc passes
-(prof_fetch, prof_write, prof_sq, prof_sq2), writes
+Reads gpurun_out/<tag>/kt (kernel trace + stats) and the separate --pmc passes
+(fetch, write, sq, sq2), writes
   profiles/<tag>_kernel_stats.csv   (copy of rocprofv3's kernel_stats)
-  profiles/<tag>_step_kernel_rocprof.md
-and updates profiles/traffic.json with the step kernel's per-launch HBM bytes:
-2 x FETCH_SIZE + WRITE_SIZE (KB -> B; gfx950 FETCH_SIZE counts half the bytes
-of 16-B/lane streamed reads, MI355X_MICROARCH.md § HBM).
+  profiles/<tag>_rocprof.md         (stats table, step-kernel PMC, roofline)
+and records the step kernel's per-launch HBM bytes 2 x FETCH_SIZE + WRITE_SIZE
+(KB -> B; gfx950 FETCH_SIZE counts half the bytes of 16-B/lane streamed reads,
+MI355X_MICROARCH.md § HBM) in profiles/traffic.json under KEY, together with
+the SHA-256 of the liblnw.so measured (bench.py reports the figure only for
+that same library).
 
-usage: python tools/rocprof_summary.py TAG [--key reference_e65536_los0_mv0]
+usage: python tools/rocprof_summary.py TAG --key reference_e65536_los0_mv0 --cmd "..."
 """
 import csv
 import json
@@ -20,6 +22,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
+sys.path.insert(0, ROOT)
 PROF = os.path.join(ROOT, "profiles")
 
 
@@ -47,51 +50,63 @@ def counters(d, stem):
 
 
 def main():
+    import hashlib
+    import bench
     tag = sys.argv[1]
-    key = "reference_e65536_los0_mv0"
-    if "--key" in sys.argv:
-        key = sys.argv[sys.argv.index("--key") + 1]
-    stats = os.path.join(OUT, "prof_kt", "kt_kernel_stats.csv")
+    key = sys.argv[sys.argv.index("--key") + 1]
+    cmd = sys.argv[sys.argv.index("--cmd") + 1] if "--cmd" in sys.argv else "bench.py"
+    d = os.path.join(OUT, tag)
+    stats = os.path.join(d, "kt", "kt_kernel_stats.csv")
     shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
-    lines = [f"# rocprofv3 --kernel-trace --stats: python3 bench.py --steps 200 --warmup 20 "
-             f"--no-cpu-baseline ({tag})", "",
+    lines = [f"# rocprofv3 --kernel-trace --stats: python3 {cmd}", "",
              "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
-    step_avg = None
+    step_avg, step_name = None, None
     for r in rows:
         avg = float(r["AverageNs"]) / 1e3
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {avg:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
                      f"{float(r['MaxNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
         if "step_kernel" in r["Name"] and step_avg is None:
-            step_avg = avg
+            step_avg, step_name = avg, short(r["Name"])
     pmc = {}
-    for d, stem in (("prof_fetch", "fetch"), ("prof_write", "write"), ("prof_sq", "sq"), ("prof_sq2", "sq2")):
-        pmc.update(counters(d, stem))
-    lines += ["", "## step_kernel PMC (per launch, mean over launches; separate --pmc passes)", ""]
+    for sub in ("fetch", "write", "sq", "sq2"):
+        pmc.update(counters(os.path.join(tag, sub), sub))
+    lines += ["", f"## {step_name} PMC (per launch, mean over launches; separate --pmc passes)", ""]
     for k in sorted(pmc):
         lines.append(f"- {k}: {pmc[k]:,.0f}")
-    E = 65536
-    alg = 2864 * E
+    parts = key.split("_")
+    E = int(parts[1][1:])
+    nb, nr = (8, 10) if parts[0] == "config4" else (4, 4)
+    B = bench.algorithmic_bytes(nb, nr)
+    alg = B * E
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         fetch, write = pmc["FETCH_SIZE"] * 1024, pmc["WRITE_SIZE"] * 1024
         traffic = 2 * fetch + write
-        lines += ["", f"HBM traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE = {traffic / 1e6:.1f} MB "
-                      f"(FETCH {fetch / 1e6:.1f} MB raw, WRITE {write / 1e6:.1f} MB); algorithmic "
-                      f"{alg / 1e6:.1f} MB (2864 B/env-step x {E})"]
+        lines += ["", f"HBM traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE = {traffic / 1e6:.2f} MB "
+                      f"(FETCH {fetch / 1e6:.2f} MB raw, WRITE {write / 1e6:.2f} MB); algorithmic "
+                      f"{alg / 1e6:.2f} MB ({B} B/env-step x {E}); ratio {traffic / alg:.3f}"]
         tf = os.path.join(PROF, "traffic.json")
         tj = json.load(open(tf)) if os.path.exists(tf) else {}
-        tj[key] = traffic
-        tj["_note"] = ("HBM bytes per step_kernel launch = 2*FETCH_SIZE + WRITE_SIZE from rocprofv3 PMC "
-                       f"(profiles/{tag}_step_kernel_rocprof.md)")
+        with open(os.path.join(ROOT, "littoral-naval-warfare-marl_amd", "lnw", "liblnw.so"), "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()
+        if tj.get("lib_sha256") != sha:
+            tj = {"lib_sha256": sha, "launch_bytes": {}}
+        tj.setdefault("launch_bytes", {})[key] = traffic
+        tj["_note"] = ("HBM bytes per step_kernel launch = 2*FETCH_SIZE + WRITE_SIZE from rocprofv3 PMC, "
+                       "for the liblnw.so with this SHA-256 (tools/gpu/prof.sh, profiles/*_rocprof.md)")
         json.dump(tj, open(tf, "w"), indent=1)
     if "SQ_WAVES" in pmc and "SQ_INSTS_VALU" in pmc:
         w = pmc["SQ_WAVES"]
         lines.append(f"VALU instructions per wave: {pmc['SQ_INSTS_VALU'] / w:,.0f}; LDS instructions per wave: "
-                     f"{pmc.get('SQ_INSTS_LDS', 0) / w:,.0f} ({w:,.0f} waves: 2 per workgroup)")
+                     f"{pmc.get('SQ_INSTS_LDS', 0) / w:,.0f} ({w:,.0f} waves)")
+        if "SQ_WAVE_CYCLES" in pmc and "SQ_WAIT_INST_ANY" in pmc:
+            lines.append(f"SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES = {pmc['SQ_WAIT_INST_ANY'] / pmc['SQ_WAVE_CYCLES']:.2f}; "
+                         f"SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES = "
+                         f"{pmc.get('SQ_ACTIVE_INST_VALU', 0) / pmc['SQ_WAVE_CYCLES']:.2f}")
     if step_avg:
-        lines.append(f"step_kernel average duration {step_avg:.1f} us -> {alg / (step_avg * 1e-6) / 1e9:.0f} GB/s "
-                     "algorithmic")
-    open(os.path.join(PROF, f"{tag}_step_kernel_rocprof.md"), "w").write("\n".join(lines) + "\n")
+        lines.append(f"{step_name} average duration {step_avg:.1f} us -> {alg / (step_avg * 1e-6) / 1e9:.0f} GB/s "
+                     f"algorithmic = {alg / (step_avg * 1e-6) / 8e12:.3f} of 8 TB/s")
+    open(os.path.join(PROF, f"{tag}_rocprof.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
