@@ -203,7 +203,8 @@ def measured_traffic(args, E):
             sha = hashlib.sha256(f.read()).hexdigest()
         if tj.get("lib_sha256") != sha:
             return None
-        return tj.get("launch_bytes", {}).get(f"{args.spawns}_e{E}_los{args.los_mode}_mv{args.move_mode}")
+        wl = "config4" if args.workload == "config4" else args.spawns
+        return tj.get("launch_bytes", {}).get(f"{wl}_e{E}_los{args.los_mode}_mv{args.move_mode}")
     except (OSError, ValueError):
         return None
 
