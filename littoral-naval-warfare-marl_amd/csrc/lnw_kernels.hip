@@ -14,6 +14,7 @@
 //   W  coalesced store of the state (or of an in-kernel auto-reset)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -220,6 +221,14 @@ struct Ctx {
   // v = own ship i at its new cell. Valid when `pre` is set.
   uint64_t lpre[2];
   bool pre;
+  // the lane that makes the env's shared-counter side effects (analytics
+  // records and maps): every lane where one lane steps one env; the first lane
+  // of the env's group in the group kernel (lnw_group.inc), whose other lanes
+  // repeat the env's serial work in step
+  bool leader = true;
+#ifdef LNW_GROUP_PROF
+  unsigned long long gp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // group-kernel section timers
+#endif
   __device__ double duct() const { return duct_col[lane]; }
 };
 
@@ -1288,7 +1297,7 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
       hit = u2 < hit_sel(P.hit64, hp, n);
     missile = true;
   }
-  if (hit) {
+  if (hit && X.leader) {
     const KState &S = X.S;
     if (missile) {  // combatant.py:642-652: maps of the trained side, launch sites of both
       if (side == (P.side_blue ? 0 : 1)) {
@@ -1300,6 +1309,8 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
     if (S.ana.eng_log)  // combatant.py:656-657
       ana_record(S.ana.eng_log, S.ana.eng_count, S.ana.eng_cap, (uint32_t)(P.env_base + X.env),
                  (uint32_t)X.step | (uint32_t)side << 16 | (uint32_t)n << 24, pa, pt);
+  }
+  if (hit) {
     int ts = t >= P.nb;
     N.cnt[ts]++;
     N.mask[ts] |= 1u << (t - (ts ? P.nb : 0));
@@ -2445,6 +2456,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
 }
 
+#include "lnw_group.inc"
+
 // ---------------------------------------------------------------------------
 // observe kernel (ship.get_obs() for a selection of ships)
 // ---------------------------------------------------------------------------
@@ -2712,7 +2725,7 @@ struct lnw_handle {
   unsigned long long *ctr = nullptr;     // bound work counters (lnw_set_counters)
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
-  bool prof = false, force_generic = false;
+  bool prof = false, force_generic = false, no_group = false, group_fits = false;
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
@@ -2830,6 +2843,17 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
     if (r[3] > tend0) tend0 = r[3];
   }
   const double us = 0.01;  // 100 MHz ticks
+  {  // spread of the per-workgroup phase-S spans (slot 1 -> 2)
+    std::vector<double> sv;
+    for (int w = 0; w < nwg; w++) {
+      const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+      if (r[2] > r[1]) sv.push_back((double)(r[2] - r[1]) * 0.01);
+    }
+    std::sort(sv.begin(), sv.end());
+    if (!sv.empty())
+      fprintf(stderr, "[lnw prof] phase S span per workgroup: p10 %.1f, p50 %.1f, p90 %.1f, max %.1f us\n",
+              sv[sv.size() / 10], sv[sv.size() / 2], sv[sv.size() * 9 / 10], sv.back());
+  }
   fprintf(stderr, "[lnw prof] wg=%d mean L %.2f us, M %.2f us, S %.2f us, W %.2f us, wave1 end-from-start %.2f us; "
                   "grid: last wave0 end %.2f us, last wave1 end %.2f us after first start\n",
           nwg, sL / nwg * us, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
@@ -2885,6 +2909,8 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   if (const char *dbg = getenv("LNW_DEBUG_SKIP")) h->dbg_skip = atoi(dbg);
   h->prof = getenv("LNW_PROF") != nullptr;
   h->force_generic = getenv("LNW_FORCE_GENERIC") != nullptr;
+  // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
+  h->no_group = getenv("LNW_NO_GROUP") != nullptr;
   h->params = *params;
   h->E = n_envs; h->nb = nb; h->nr = nr; h->A = nb + nr;
   h->nmax = nb > nr ? nb : nr;
@@ -3018,14 +3044,22 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   {
     size_t need = step_lds_bytes(h) + 1024;
     if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
-    if (need > 64 * 1024) {
-      const void *ks[9] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
-                           (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
-                           (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
-                           (const void *)step_kernel<4, 4, true>, (const void *)step_kernel<0, 0, false, true>,
-                           (const void *)observe_kernel};
+    bool atan_lds;
+    const size_t gneed = (size_t)group_lds_bytes((int)step_lds_bytes(h), h->nb * h->nr, atan_lds) + 1024;
+    h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX;  // else runtime sizes stay on step_kernel<0, 0>
+    // the limit is per kernel function, shared by every handle of the process:
+    // set to the CU's whole LDS once, so a smaller handle never lowers it under
+    // a larger one's launch (the launch's own size sets the occupancy)
+    static bool lds_opt_in = false;
+    if (!lds_opt_in && (need > 64 * 1024 || gneed > 64 * 1024)) {
+      const void *ks[10] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
+                            (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
+                            (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
+                            (const void *)step_kernel<4, 4, true>, (const void *)step_kernel<0, 0, false, true>,
+                            (const void *)observe_kernel,          (const void *)step_group_kernel};
       for (const void *kk : ks)
-        HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+        HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, GROUP_LDS_MAX));
+      lds_opt_in = true;
     }
   }
   (void)hipGetLastError();
@@ -3115,6 +3149,14 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
   else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
   else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
+  else if (!generic && !h->no_group && h->group_fits) {
+    // runtime team sizes: GL lanes per env (lnw_group.inc)
+    bool atan_lds;
+    const size_t glds = (size_t)group_lds_bytes((int)lds, h->nb * h->nr, atan_lds);
+    step_group_kernel<<<dim3((h->E + GEPW - 1) / GEPW), dim3(GEPW * GL), glds, st>>>(
+        k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev,
+        done_dev, cog_dev);
+  }
   else LNW_STEP(0, 0, false, false);
 #undef LNW_STEP
   HIPCHK(hipGetLastError());

@@ -16,6 +16,7 @@ INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "liblnw.so")
 SOURCES = [os.path.join(CSRC, "lnw_kernels.hip"), os.path.join(CSRC, "lnw_actor.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "lnw_device.h"), os.path.join(CSRC, "lnw_quiet.inc"),
+                  os.path.join(CSRC, "lnw_group.inc"),
                   os.path.join(INCLUDE, "lnw.h")]
 
 
@@ -31,20 +32,21 @@ def flags(arch="gfx950"):
             "-fno-gpu-flush-denormals-to-zero", "-fPIC", "-shared", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
-def build(force=False, verbose=False):
-    if not force and os.path.exists(OUT):
-        t = os.path.getmtime(OUT)
+def build(force=False, verbose=False, out=OUT, defines=()):
+    """liblnw.so (or a diagnostics variant at `out` built with -D`defines`)."""
+    if not force and os.path.exists(out):
+        t = os.path.getmtime(out)
         if all(os.path.getmtime(d) <= t for d in DEPS):
-            return OUT
-    cmd = [hipcc()] + flags() + SOURCES + ["-o", OUT + ".tmp"]
+            return out
+    cmd = [hipcc()] + flags() + [f"-D{d}" for d in defines] + SOURCES + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("hipcc failed building liblnw.so")
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
