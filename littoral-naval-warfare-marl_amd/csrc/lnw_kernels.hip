@@ -2461,6 +2461,11 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
 // ---------------------------------------------------------------------------
 // observe kernel (ship.get_obs() for a selection of ships)
 // ---------------------------------------------------------------------------
+// NB/NR > 0: compile-time team sizes — every LOS word the calls need loaded in
+// one batch (los_prefetch_t: no ship moves here, so only the current cells) and
+// the templated get_obs (get_obs_t; CW: the contact variant's mask walk), as
+// the step kernel's phase S; NB = NR = 0: runtime sizes (get_obs_dev).
+template <int NB = 0, int NR = 0, bool CW = false>
 __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
                                                      float *obs_r) {
   const int lane = threadIdx.x & (WAVE - 1);
@@ -2476,7 +2481,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   __shared__ double duct_col[WAVE];
   for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
   const uint32_t *mask = c.mask;
-  load_state<0, 1>(P, S, c, lane, env, valid, 0);
+  load_state<NB + NR, 1>(P, S, c, lane, env, valid, 0);
   double duct = valid ? S.duct[env] : 1.0;
   duct_col[lane] = duct;
   __syncthreads();
@@ -2487,10 +2492,18 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
     if (sel >= 0) { a0 = sel; a1 = sel + 1; }
     else if (sel == LNW_OBS_BLUE) { a1 = nb; }
     else if (sel == LNW_OBS_RED) { a0 = nb; }
+    if constexpr (NB > 0) {
+      if (P.los_mode != 1) los_prefetch_t<NB, NR>(X);
+    }
     for (int a = a0; a < a1; a++) {
       if (!COLB(c.alive0, a)) continue;
-      if (P.los_mode == 2) march_pairs_ref(X, a);
-      get_obs_dev(X, a);
+      if constexpr (NB > 0) {
+        if (a < NB) get_obs_t<NB, NR, CW>(X, a, 0, NB);
+        else get_obs_t<NR, NB, CW>(X, a, NB, 0);
+      } else {
+        if (P.los_mode == 2) march_pairs_ref(X, a);
+        get_obs_dev(X, a);
+      }
       COLB(c.obsd, a) = 1;
       S.tl_cnt[(size_t)a * E + env] = (uint16_t)COLW(c.tcnt, a);
     }
@@ -3052,11 +3065,14 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     // a larger one's launch (the launch's own size sets the occupancy)
     static bool lds_opt_in = false;
     if (!lds_opt_in && (need > 64 * 1024 || gneed > 64 * 1024)) {
-      const void *ks[10] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
+      const void *ks[16] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
                             (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
                             (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
                             (const void *)step_kernel<4, 4, true>, (const void *)step_kernel<0, 0, false, true>,
-                            (const void *)observe_kernel,          (const void *)step_group_kernel};
+                            (const void *)observe_kernel<0, 0, false>, (const void *)step_group_kernel,
+                            (const void *)observe_kernel<2, 2, false>, (const void *)observe_kernel<3, 3, false>,
+                            (const void *)observe_kernel<4, 4, false>, (const void *)observe_kernel<2, 2, true>,
+                            (const void *)observe_kernel<3, 3, true>, (const void *)observe_kernel<4, 4, true>};
       for (const void *kk : ks)
         HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, GROUP_LDS_MAX));
       lds_opt_in = true;
@@ -3171,7 +3187,16 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
   KState s = make_state(h);
   size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + h->kp.epw - 1) / h->kp.epw), block(WAVE);
-  observe_kernel<<<grid, block, lds, (hipStream_t)stream>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev);
+  hipStream_t st = (hipStream_t)stream;
+  const bool tmpl = !h->force_generic && h->params.los_mode != 2 && h->nb == h->nr;
+  const bool cw = h->contact;
+#define LNW_OBS(NB_, CW_) \
+  observe_kernel<NB_, NB_, CW_><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev)
+  if (tmpl && h->nb == 4) { if (cw) LNW_OBS(4, true); else LNW_OBS(4, false); }
+  else if (tmpl && h->nb == 3) { if (cw) LNW_OBS(3, true); else LNW_OBS(3, false); }
+  else if (tmpl && h->nb == 2) { if (cw) LNW_OBS(2, true); else LNW_OBS(2, false); }
+  else LNW_OBS(0, false);
+#undef LNW_OBS
   HIPCHK(hipGetLastError());
   return 0;
 }

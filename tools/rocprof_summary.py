@@ -28,7 +28,7 @@ PROF = os.path.join(ROOT, "profiles")
 
 def short(name):
     n = name.replace("(anonymous namespace)::", "").replace("void ", "")
-    if n.startswith("step_kernel"):
+    if n.startswith("step_kernel") and ">" in n:
         return n[: n.index(">") + 1]
     return n.split("(")[0]
 
@@ -40,7 +40,7 @@ def counters(d, stem):
         return {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "step_kernel" not in r["Kernel_Name"]:
+            if "step_kernel" not in r["Kernel_Name"] and "step_group_kernel" not in r["Kernel_Name"]:
                 continue
             acc[(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
     per = defaultdict(list)
@@ -66,7 +66,7 @@ def main():
         avg = float(r["AverageNs"]) / 1e3
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {avg:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
                      f"{float(r['MaxNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
-        if "step_kernel" in r["Name"] and step_avg is None:
+        if ("step_kernel" in r["Name"] or "step_group_kernel" in r["Name"]) and step_avg is None:
             step_avg, step_name = avg, short(r["Name"])
     pmc = {}
     for sub in ("fetch", "write", "sq", "sq2"):
