@@ -85,6 +85,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
                    help="threads for the CPU baseline (the GPU box's share is 16 cores)")
+    p.add_argument("--episode-steps", type=int, default=40,
+                   help="episode horizon (config.json: 40); diagnostics only")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary lines (configs 2, 3-shard, 4, 5, melee, march)")
     p.add_argument("--secondary-steps", type=int, default=100)
@@ -95,12 +97,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+EPISODE_STEPS = 40  # config.json hyperparameters.episode_steps
+
+
 def make_game(E, env_base, spawns, los_mode, move_mode, cfg=None):
     from lnw.batched import BatchedGame, default_grid
     from lnw.config import Scenario
     if cfg is None:
         sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=True,
-                      auto_reset=True, episode_steps=40, los_mode=los_mode, move_mode=move_mode)
+                      auto_reset=True, episode_steps=EPISODE_STEPS, los_mode=los_mode,
+                      move_mode=move_mode)
         g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc,
                         device=torch.cuda.current_device(), env_id_base=env_base, seed=1234)
         # melee: fleets in contact every step -> the contact variant of the
@@ -381,6 +387,8 @@ def secondary_lines(args):
 
 def main():
     args = parse()
+    global EPISODE_STEPS
+    EPISODE_STEPS = args.episode_steps
     from lnw import dist
     world, rank, local = dist.world()
     # LNW_FORCE_DEVICE / LNW_DIST_BACKEND: the multi-rank test runs two ranks on

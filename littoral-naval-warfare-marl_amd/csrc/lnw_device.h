@@ -130,6 +130,92 @@ __device__ inline double u53(uint32_t a, uint32_t b) {
 
 // Portable ln and cos(2*pi*u): only + - * / and frexp, identical bits on the CPU
 // oracle and the GPU (production-mode gauss draws).
+// tan(x) for |x| < 2^19 * pi/2 (EW-fix slopes, combatant.py:270-271): the
+// fdlibm algorithm — rem_pio2's medium path (x - n*pi/2 with pi/2 in three
+// 33-bit pieces) and __kernel_tan's degree-25 odd polynomial with the
+// pi/4 - x reflection above 0.6744 — in plain IEEE double arithmetic
+// (error < 1 ulp, like the library tan it replaces; tools/tan_probe.hip
+// compares it with the host libm over the bearing domain).
+__host__ __device__ inline unsigned long long tan_bits(double x) { return __builtin_bit_cast(unsigned long long, x); }
+__host__ __device__ inline double tan_from_bits(unsigned long long b) { return __builtin_bit_cast(double, b); }
+__host__ __device__ inline double tan_kernel_fd(double x, double y, int iy) {
+  const double T0 = 3.33333333333334091986e-01, T1 = 1.33333333333201242699e-01,
+               T2 = 5.39682539762260521377e-02, T3 = 2.18694882948595424599e-02,
+               T4 = 8.86323982359930005737e-03, T5 = 3.59207910759131235356e-03,
+               T6 = 1.45620945432529025516e-03, T7 = 5.88041240820264096874e-04,
+               T8 = 2.46463134818469906812e-04, T9 = 7.81794442939557092300e-05,
+               T10 = 7.14072491382608190305e-05, T11 = -1.85586374855275456654e-05,
+               T12 = 2.59073051863633712884e-05;
+  const double pio4 = 7.85398163397448278999e-01, pio4lo = 3.06161699786838301793e-17;
+  const int hx = (int)(tan_bits(x) >> 32), ix = hx & 0x7fffffff;
+  if (ix < 0x3e300000) {  // |x| < 2^-28
+    if (iy == 1) return x;
+    return -1.0 / x;      // (x == 0 never reaches here with iy = -1 from a reduction)
+  }
+  const bool big = ix >= 0x3FE59428;  // |x| >= 0.6744
+  if (big) {
+    if (hx < 0) { x = -x; y = -y; }
+    const double z = pio4 - x, w = pio4lo - y;
+    x = z + w;
+    y = 0.0;
+  }
+  double z = x * x, w = z * z;
+  double r = T1 + w * (T3 + w * (T5 + w * (T7 + w * (T9 + w * T11))));
+  double v = z * (T2 + w * (T4 + w * (T6 + w * (T8 + w * (T10 + w * T12)))));
+  double s = z * x;
+  r = y + z * (s * (r + v) + y);
+  r += T0 * s;
+  w = x + r;
+  if (big) {
+    v = (double)iy;
+    return (double)(1 - ((hx >> 30) & 2)) * (v - 2.0 * (x - (w * w / (w + v) - r)));
+  }
+  if (iy == 1) return w;
+  // -1 / (x + r) accurately
+  const double zz = tan_from_bits(tan_bits(w) & 0xffffffff00000000ull);
+  v = r - (zz - x);
+  const double a = -1.0 / w;
+  const double t = tan_from_bits(tan_bits(a) & 0xffffffff00000000ull);
+  s = 1.0 + t * zz;
+  return t + a * (s + t * v);
+}
+__host__ __device__ inline double tan_fd(double x) {
+  const int ix = (int)(tan_bits(x) >> 32) & 0x7fffffff;
+  if (ix <= 0x3fe921fb) return tan_kernel_fd(x, 0.0, 1);  // |x| ~<= pi/4
+  if (ix >= 0x7ff00000) return x - x;                      // inf / nan
+  // rem_pio2, medium path (|x| < 2^19 * pi/2 here: bearings in degrees < 1e5)
+  const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+               pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
+               pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+               pio2_3t = 8.47842766036889956997e-32;
+  const double t = fabs(x);
+  const int n = (int)(t * invpio2 + 0.5);
+  const double fn = (double)n;
+  double r = t - fn * pio2_1, w = fn * pio2_1t;  // first round: good to 85 bits
+  const int j = ix >> 20;
+  double y0 = r - w;
+  int i = j - (int)((tan_bits(y0) >> 52) & 0x7ff);
+  if (i > 16) {  // second round: good to 118 bits
+    double tt = r;
+    w = fn * pio2_2;
+    r = tt - w;
+    w = fn * pio2_2t - ((tt - r) - w);
+    y0 = r - w;
+    i = j - (int)((tan_bits(y0) >> 52) & 0x7ff);
+    if (i > 49) {  // third round: 151 bits
+      tt = r;
+      w = fn * pio2_3;
+      r = tt - w;
+      w = fn * pio2_3t - ((tt - r) - w);
+      y0 = r - w;
+    }
+  }
+  double y1 = (r - y0) - w;
+  int nn = n;
+  if (x < 0) { y0 = -y0; y1 = -y1; nn = -n; }
+  return tan_kernel_fd(y0, y1, 1 - ((nn & 1) << 1));
+}
+
 __device__ inline double p_log(double x) {
   int e;
   double m = frexp(x, &e);

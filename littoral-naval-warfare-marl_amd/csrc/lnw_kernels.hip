@@ -506,8 +506,8 @@ __device__ inline bool fix_mean_loop(Ctx &X, int jj, int n, double &mx, double &
     uint8_t s1 = S.bear_ship[slot(k)], s2 = S.bear_ship[slot(k + 1)];
     double b1 = S.bear_val[slot(k)], b2 = S.bear_val[slot(k + 1)];
     uint32_t p1 = COLW(c.pos_cur, s1), p2 = COLW(c.pos_cur, s2);
-    double m1 = tan(b1 * DEG2RAD);
-    double m2 = tan(b2 * DEG2RAD);
+    double m1 = tan_fd(b1 * DEG2RAD);
+    double m2 = tan_fd(b2 * DEG2RAD);
     if (m1 - m2 == 0.0) return false;
     double x3, y3;
     fix_pair(m1, m2, pos_x(p1), pos_y(p1), pos_x(p2), pos_y(p2), x3, y3);
@@ -539,7 +539,7 @@ __device__ inline bool fix_mean_batched(Ctx &X, int jj, int n, double &mx, doubl
     tv[k] = 0.0;
     px[k] = py[k] = 0.0;
     if (k < n) {
-      tv[k] = tan(bv[k] * DEG2RAD);
+      tv[k] = tan_fd(bv[k] * DEG2RAD);
       const uint32_t p = COLW(c.pos_cur, bs[k]);
       px[k] = pos_x(p);
       py[k] = pos_y(p);
@@ -914,7 +914,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
     // calculate_bearing (combatant.py:249-263)
     const double br1 = a1 + g1 < 0 ? a1 + g1 + 360.0 : a1 + g1;
     const double br2 = a2 + g2 < 0 ? a2 + g2 + 360.0 : a2 + g2;
-    const double m1 = tan(br1 * DEG2RAD), m2 = tan(br2 * DEG2RAD);
+    const double m1 = tan_fd(br1 * DEG2RAD), m2 = tan_fd(br2 * DEG2RAD);
     accum(j1, m1, x1, y1);
     if (two) accum(j2, m2, x2, y2);
   }
@@ -933,7 +933,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
     const int k = __builtin_popcount(bearm & ((1u << b) - 1u));
     const double g = X.rng.gauss_at(base + (unsigned long long)k);
     const double bearing = a0 + g < 0 ? a0 + g + 360.0 : a0 + g;  // calculate_bearing (combatant.py:249-263)
-    const double m = tan(bearing * DEG2RAD);
+    const double m = tan_fd(bearing * DEG2RAD);
     const double x1 = pos_x(pi), y1 = pos_y(pi);
     if (cnt > 0 && !zero) {
       if (mprev - m == 0.0) {
