@@ -208,8 +208,10 @@ int lnw_set_variant(lnw_handle *h, int32_t contact);
  * (queries outside the LOS table, or every query with los_mode = 1), to [1] the
  * Bresenham cells those rays visit (combatant.py:411-456) and to [2] the A*
  * searches they run (targets outside the move table, or move_mode = 1;
- * combatant.py:289-408). counters_dev: [4] uint64 device array, or NULL to
- * unbind. Costs one uniform branch per march / search while unbound. */
+ * combatant.py:289-408), to [3] the EW bearings the contact variant evaluates
+ * in wave-pooled rounds (get_obs calls whose busiest lane has more than two).
+ * counters_dev: [4] uint64 device array, or NULL to unbind. Costs one uniform
+ * branch per march / search / pooled get_obs while unbound. */
 int lnw_set_counters(lnw_handle *h, uint64_t *counters_dev);
 
 /* Reward / cog output type of lnw_step. f64 = 0 (default): rew_blue, rew_red and

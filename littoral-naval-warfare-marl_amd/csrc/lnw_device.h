@@ -314,7 +314,12 @@ struct Rng {
       const long long p = tape_lo + (long long)c;
       return p < tape_hi ? tape[p] : 0.0;
     }
-    uint32_t o[4] = {(uint32_t)c, (uint32_t)(c >> 32), g0, g1};
+    return gauss_philox(c, g0, g1);
+  }
+  // the Philox gauss draw c of the stream keyed (k0, k1, h0, h1): another env's
+  // draw (h0, h1 = its global env id) in the pooled bearings of finish_obs_t
+  __device__ double gauss_philox(unsigned long long c, uint32_t h0, uint32_t h1) const {
+    uint32_t o[4] = {(uint32_t)c, (uint32_t)(c >> 32), h0, h1};
     philox10(o, k0, k1);
     double a = u53(o[0], o[1]), b = u53(o[2], o[3]);
     return sqrt(-2.0 * p_log(1.0 - a)) * p_cos2pi(b);

@@ -816,7 +816,8 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
     }
   }
   tq = prof_acc(S, 21, tq);
-  if (bearm == 0) { COLW(c.tcnt, me) = (uint32_t)tn; return; }
+  // (contact variant: lanes without bearings stay, to evaluate other lanes' bearings)
+  if (!CW && bearm == 0) { COLW(c.tcnt, me) = (uint32_t)tn; return; }
   uint32_t colj = 0;  // bits of opponent 0's column
 #pragma unroll
   for (int i = 0; i < NOWN; i++) colj |= 1u << (i * NOPP);
@@ -830,6 +831,20 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
     if (__builtin_popcount(bj) < 2) continue;
 #pragma unroll
     for (int i = 0; i < NOWN; i++) need |= ((bj >> (i * NOPP + j)) & 1u) << (j * NOWN + i);
+  }
+  if (S.prof) {  // bearing load balance: lane sum and wave max of the bearings evaluated
+    const int cnt = __builtin_popcount(need);
+    int s = 0, mx = 0;  // over the active lanes, by ballots
+    for (int b = 4; b >= 0; b--) {
+      s += __popcll(__ballot((cnt >> b) & 1)) << b;
+      if (__ballot(cnt >= (mx | (1 << b)))) mx |= 1 << b;
+    }
+    const unsigned long long m = __ballot(1);
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)m) - 1) {
+      atomicAdd(&S.prof[(size_t)blockIdx.x * PROF_SLOTS + 24], (unsigned long long)s);
+      atomicAdd(&S.prof[(size_t)blockIdx.x * PROF_SLOTS + 25], (unsigned long long)mx);
+      atomicAdd(&S.prof[(size_t)blockIdx.x * PROF_SLOTS + 26], (unsigned long long)__popcll(m));
+    }
   }
   int fxr[NOPP], fyr[NOPP];
 #pragma unroll
@@ -893,6 +908,112 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
     cnt++;
     mprev = m; xprev = x1; yprev = y1;
   };
+  // wave max of the per-lane bearing counts (ballots over the active lanes)
+  const unsigned long long act = __ballot(1);
+  const int ncnt = __builtin_popcount(need);
+  int wmax = 0;
+#pragma unroll
+  for (int b = 4; b >= 0; b--)
+    if (__ballot(ncnt >= (wmax | (1 << b)))) wmax |= 1 << b;
+  if (wmax > 2 && !(P.dbg_skip & 131072)) {  // (LNW_DEBUG_SKIP bit 17: per-lane loop)
+    // Pooled: the wave's bearings are numbered lane by lane (lane l's k-th
+    // bearing is g = excl_l + k) and every active lane evaluates two of them per
+    // round, g = r0 + rank and r0 + nact + rank, so a round costs the same
+    // whichever lanes own them (the per-lane loop runs the busiest lane's
+    // count). Each owner then takes its slopes, in its own order, by shuffles and
+    // sums its fixes as below: identical arithmetic.
+    const int nact = __popcll(act);
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    int excl = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+      const unsigned long long bb = __ballot((ncnt >> b) & 1);
+      excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32),
+                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+      total += __popcll(bb) << b;
+    }
+    if (S.ctr && rank == 0) atomicAdd(&S.ctr[3], (unsigned long long)total);  // work counter
+    // rank -> lane and rank -> first bearing number, in the observed-list
+    // columns (unused by the contact variant's walk)
+    uint8_t *lor = (uint8_t *)c.observed;
+    uint16_t *exr = (uint16_t *)(lor + WAVE);
+    lor[rank] = (uint8_t)lane;
+    exr[rank] = (uint16_t)excl;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool tape = X.rng.mode == 1;
+    // bearing g's owner (the last rank whose first number is <= g), its pair and
+    // its tangent; the shuffles run on every active lane (owners are active)
+    auto locate = [&](int g, int &s, uint32_t &pi, uint32_t &pj, unsigned long long &drw) {
+      int lo = 0;
+#pragma unroll
+      for (int st = 32; st; st >>= 1)
+        if (lo + st < nact && (int)exr[lo + st] <= g) lo += st;
+      s = lor[lo];
+      const int kk = g - (int)exr[lo];
+      uint32_t ns = (uint32_t)__shfl((int)need, s);
+      const uint32_t bs = (uint32_t)__shfl((int)bearm, s);
+      drw = __shfl(base, s);
+      for (int q = 0; q < kk; q++) ns &= ns - 1;
+      const int t = __builtin_ctz(ns);
+      const int j = t / NOWN, i = t - j * NOWN, b = i * NOPP + j;
+      drw += (unsigned long long)__builtin_popcount(bs & ((1u << b) - 1u));
+      pi = c.pos_cur[(own0 + i) * PAD + s];
+      pj = c.pos_cur[(opp0 + j) * PAD + s];
+    };
+    auto draw = [&](int s, unsigned long long d) -> double {
+      const int es = env - lane + s;
+      if (tape) {
+        if (!S.tape_off) return 0.0;
+        const long long p = S.tape_off[es] + (long long)d;
+        return p < S.tape_off[es + 1] ? S.tape[p] : 0.0;
+      }
+      const unsigned long long gid = (unsigned long long)(P.env_base + es);
+      return X.rng.gauss_philox(d, (uint32_t)gid, (uint32_t)(gid >> 32));
+    };
+    int myg = excl;
+    uint32_t myn = need;
+    for (int r0 = 0; r0 < total; r0 += 2 * nact) {
+      const int g1 = min(r0 + rank, total - 1), g2 = min(r0 + nact + rank, total - 1);
+      int s1, s2;
+      uint32_t pi1, pj1, pi2, pj2;
+      unsigned long long d1, d2;
+      locate(g1, s1, pi1, pj1, d1);
+      locate(g2, s2, pi2, pj2, d2);
+      const int dx1 = pos_x(pj1) - pos_x(pi1), dy1 = pos_y(pj1) - pos_y(pi1);
+      const int dx2 = pos_x(pj2) - pos_x(pi2), dy2 = pos_y(pj2) - pos_y(pi2);
+      const BearPre b1 = bearing_pre(P, S, dx1, dy1), b2 = bearing_pre(P, S, dx2, dy2);
+      double a1 = b1.v, a2 = b2.v;
+      if (!(b1.tab && b2.tab)) {
+        a1 = bearing_use(b1, dx1, dy1);
+        a2 = bearing_use(b2, dx2, dy2);
+      }
+      const double gg1 = draw(s1, d1), gg2 = draw(s2, d2);
+      // calculate_bearing (combatant.py:249-263)
+      const double br1 = a1 + gg1 < 0 ? a1 + gg1 + 360.0 : a1 + gg1;
+      const double br2 = a2 + gg2 < 0 ? a2 + gg2 + 360.0 : a2 + gg2;
+      const double m1 = tan_fd(br1 * DEG2RAD), m2 = tan_fd(br2 * DEG2RAD);
+      // owners take this round's slopes of their bearings, in order
+      const int rend = r0 + 2 * nact;
+      for (;;) {
+        const bool more = myn != 0 && myg < rend;
+        if (!__ballot(more)) break;
+        const int off = myg - r0;
+        const bool second = off >= nact;
+        const int src = more ? lor[(second ? off - nact : off) & (WAVE - 1)] : lane;
+        const double v1 = __shfl(m1, src), v2 = __shfl(m2, src);
+        if (more) {
+          const int t = __builtin_ctz(myn);
+          myn &= myn - 1;
+          myg++;
+          int dx, dy, j, k;
+          double x1, y1;
+          setup(t, dx, dy, j, x1, y1, k);
+          accum(j, second ? v2 : v1, x1, y1);
+        }
+      }
+    }
+  } else
   while (need) {
     const int t1 = __builtin_ctz(need);
     need &= need - 1;
@@ -2871,6 +2992,16 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
                   "grid: last wave0 end %.2f us, last wave1 end %.2f us after first start\n",
           nwg, sL / nwg * us, sM / nwg * us, sS / nwg * us, sW / nwg * us, n1 ? s1 / n1 * us : 0.0,
           (double)(tend0 - t0) * us, tend1 ? (double)(tend1 - t0) * us : 0.0);
+  {
+    double bs = 0, bm = 0, bl = 0;
+    for (int w = 0; w < nwg; w++) {
+      const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+      bs += (double)r[24]; bm += (double)r[25]; bl += (double)r[26];
+    }
+    if (bl > 0)
+      fprintf(stderr, "[lnw prof] EW bearings (contact variant): %.0f evaluated, wave max summed %.0f, "
+                      "active lanes %.0f; balanced/actual %.3f\n", bs, bm, bl, bs / 64.0 / bm);
+  }
   if (nq)
     fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us\n",
             nq, sq[0] / nq * us, sq[1] / nq * us, sq[2] / nq * us, sq[3] / nq * us);

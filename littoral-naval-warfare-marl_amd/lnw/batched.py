@@ -251,7 +251,8 @@ class BatchedGame:
 
     def count_work(self, on=True):
         """Bind (on) or unbind the device work counters (lnw_set_counters):
-        rays ray-marched, Bresenham cells visited, A* searches run."""
+        rays ray-marched, Bresenham cells visited, A* searches run, EW bearings
+        evaluated in wave-pooled rounds (contact variant)."""
         if on:
             self._ctr = torch.zeros(4, dtype=torch.int64, device=self.device)
             check(self.L.lnw_set_counters(self.h, _ptr(self._ctr)))
@@ -260,7 +261,8 @@ class BatchedGame:
 
     def work_counts(self):
         c = self._ctr.cpu().tolist()
-        return dict(rays_marched=c[0], cells_marched=c[1], astar_searches=c[2])
+        return dict(rays_marched=c[0], cells_marched=c[1], astar_searches=c[2],
+                    pooled_bearings=c[3])
 
     def observe(self, agent=-1):
         """ship.get_obs() for every live ship (agent=-1, blue then red), one side

@@ -445,6 +445,55 @@ def test_philox_4v4_vs_oracle_launch_shapes(grids, epw, contact):
     g.close()
 
 
+def test_contact_pooled_bearings(grids):
+    """Contact variant at melee spawns (every get_obs has EW bearings): the
+    wave-pooled bearing rounds (finish_obs_t) run — the work counter says so —
+    and give the same trajectories as the per-lane loop (LNW_DEBUG_SKIP bit 17)
+    and as the default variant; a sample of envs is checked against the oracle."""
+    import os
+    import _oracle
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    grid = grids[0]
+    E, S = 1024, 6
+    pos = _melee_positions(grid, E, 4, 4, seed=5)
+    rng = np.random.default_rng(7)
+    acts = [rng.random((E, 8, 4)).astype(np.float32) for _ in range(S)]
+    outs = []
+    for contact, skip in ((True, "0"), (True, str(1 << 17)), (False, "0")):
+        os.environ["LNW_DEBUG_SKIP"] = skip
+        try:
+            g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+                            grid=grid, seed=21)
+        finally:
+            os.environ.pop("LNW_DEBUG_SKIP")
+        g.set_variant(contact)
+        g.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
+        g.count_work(True)
+        traj = [{k: v.cpu().numpy().copy() for k, v in g.step(torch.from_numpy(a).cuda()).items()}
+                for a in acts]
+        torch.cuda.synchronize()
+        outs.append((traj, g.work_counts()))
+        g.close()
+    assert outs[0][1]["pooled_bearings"] > 0, outs[0][1]
+    assert outs[1][1]["pooled_bearings"] == 0 and outs[2][1]["pooled_bearings"] == 0
+    for traj, _ in outs[1:]:
+        for s in range(S):
+            for k in traj[s]:
+                assert np.array_equal(outs[0][0][s][k], traj[s][k], equal_nan=True), (s, k)
+    for e in range(0, E, 97):
+        o = _oracle.OracleEnv(grid, 4, 4)
+        o.set_philox(21, e)
+        o.reset([0] * 4 + [1] * 4, pos[e])
+        for s in range(S):
+            r = o.step(acts[s][e], np.full(8, _oracle.K_F32, np.int32))
+            out = outs[0][0][s]
+            assert np.array_equal(out["obs_blue"][e], r["obs_blue"].astype(np.float32)), (s, e)
+            assert np.array_equal(out["obs_red"][e], r["obs_red"].astype(np.float32)), (s, e)
+            assert np.allclose(out["rew_blue"][e], r["rew_blue"], rtol=0, atol=REW_TOL), (s, e)
+            assert out["done"][e] == r["done"], (s, e)
+
+
 def test_config4_launch_shape_invariance(grids):
     """Config 4 shape (8 small blue vs 8 large + 2 LandingShip red, landing ops,
     200x200 grid, box spawns): the automatic envs-per-workgroup choice, 64 and 1
@@ -705,7 +754,8 @@ def test_work_counters(grids):
         counts[mode] = g.work_counts()
         g.count_work(False)
         g.close()
-    assert counts[0] == dict(rays_marched=0, cells_marched=0, astar_searches=0), counts[0]
+    assert counts[0] == dict(rays_marched=0, cells_marched=0, astar_searches=0,
+                             pooled_bearings=0), counts[0]
     c = counts[1]
     # at most one A* per live ship per step (8 ships x 3 steps x E); at these
     # spawns the march mode's range pruning leaves no pair to march
