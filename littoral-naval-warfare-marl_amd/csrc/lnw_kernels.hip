@@ -915,13 +915,18 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
 #pragma unroll
   for (int b = 4; b >= 0; b--)
     if (__ballot(ncnt >= (wmax | (1 << b)))) wmax |= 1 << b;
-  if (wmax > 2 && !(P.dbg_skip & 131072)) {  // (LNW_DEBUG_SKIP bit 17: per-lane loop)
-    // Pooled: the wave's bearings are numbered lane by lane (lane l's k-th
-    // bearing is g = excl_l + k) and every active lane evaluates two of them per
-    // round, g = r0 + rank and r0 + nact + rank, so a round costs the same
-    // whichever lanes own them (the per-lane loop runs the busiest lane's
-    // count). Each owner then takes its slopes, in its own order, by shuffles and
-    // sums its fixes as below: identical arithmetic.
+  if (NOWN * NOPP > 2 && wmax > 2 && !(P.dbg_skip & 131072)) {  // (LNW_DEBUG_SKIP bit 17: per-lane loop)
+    // Pooled: the wave's bearings are numbered owner by owner (lane l's k-th
+    // bearing, in need-bit order, is g = excl_l + k) and every active lane takes
+    // two consecutive ones per round, g = r0 + 2 rank and g + 1, so a round costs
+    // the same whichever lanes own them (the per-lane loop runs the busiest lane's
+    // count). An opponent's bearings from one owner are consecutive numbers (a
+    // segment of at most NOWN); each slot computes its slope, the fix with the
+    // previous slot of its segment (fix_pair, the same operands as the per-lane
+    // loop), and the running sum of its segment's fixes, left to right like the
+    // per-lane loop, by a segmented scan over the slots. The segment's last slot
+    // takes the mean, rounds it and stores the fix (or the error) in an LDS table
+    // the owner reads afterwards: identical arithmetic and results.
     const int nact = __popcll(act);
     const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
@@ -934,17 +939,25 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
       total += __popcll(bb) << b;
     }
     if (S.ctr && rank == 0) atomicAdd(&S.ctr[3], (unsigned long long)total);  // work counter
-    // rank -> lane and rank -> first bearing number, in the observed-list
-    // columns (unused by the contact variant's walk)
+    // in the observed-list / bearing-order columns (unused by the contact
+    // variant's walk; >= 396 B per opponent slot, this needs 192 + 256 per
+    // opponent): rank -> lane, rank -> first bearing number, and the fix table
+    // [opponent][owner lane]: fx | fy << 8 | inside << 16 | zero-div << 17 | nan << 18
     uint8_t *lor = (uint8_t *)c.observed;
     uint16_t *exr = (uint16_t *)(lor + WAVE);
+    uint32_t *fixt = (uint32_t *)(lor + 3 * WAVE);
     lor[rank] = (uint8_t)lane;
     exr[rank] = (uint16_t)excl;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int prevl = rank > 0 ? (int)lor[rank - 1] : lane;  // the lane of the previous rank
+    const int lastl = 63 - __builtin_clzll(act);              // the lane of the last rank
     const bool tape = X.rng.mode == 1;
-    // bearing g's owner (the last rank whose first number is <= g), its pair and
-    // its tangent; the shuffles run on every active lane (owners are active)
-    auto locate = [&](int g, int &s, uint32_t &pi, uint32_t &pj, unsigned long long &drw) {
+    constexpr uint32_t SEGM = (1u << NOWN) - 1u;
+    // bearing g: owner lane s, own ship i, opponent j, the owner's bearings on j
+    // (bit i), its gauss draw number and the two positions. The shuffles run on
+    // every active lane (owners are active).
+    auto locate = [&](int g, int &s, int &i, int &j, uint32_t &nsj, unsigned long long &drw,
+                      uint32_t &pi, uint32_t &pj) {
       int lo = 0;
 #pragma unroll
       for (int st = 32; st; st >>= 1)
@@ -954,10 +967,14 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
       uint32_t ns = (uint32_t)__shfl((int)need, s);
       const uint32_t bs = (uint32_t)__shfl((int)bearm, s);
       drw = __shfl(base, s);
-      for (int q = 0; q < kk; q++) ns &= ns - 1;
-      const int t = __builtin_ctz(ns);
-      const int j = t / NOWN, i = t - j * NOWN, b = i * NOPP + j;
+      uint32_t w = ns;
+      for (int q = 0; q < kk; q++) w &= w - 1;
+      const int t = __builtin_ctz(w);
+      j = t / NOWN;
+      i = t - j * NOWN;
+      const int b = i * NOPP + j;
       drw += (unsigned long long)__builtin_popcount(bs & ((1u << b) - 1u));
+      nsj = (ns >> (j * NOWN)) & SEGM;
       pi = c.pos_cur[(own0 + i) * PAD + s];
       pj = c.pos_cur[(opp0 + j) * PAD + s];
     };
@@ -971,46 +988,111 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
       const unsigned long long gid = (unsigned long long)(P.env_base + es);
       return X.rng.gauss_philox(d, (uint32_t)gid, (uint32_t)(gid >> 32));
     };
-    int myg = excl;
-    uint32_t myn = need;
+    // mean, rounding and grid test of a finished segment (the per-lane flush)
+    auto finish = [&](int s, int j, int n, double sx, double sy, bool z, int stp) {
+      uint32_t w = 0;
+      if (z) {
+        w = 1u << 17;
+      } else {
+        const double mx = sx / (double)(n - 1), my = sy / (double)(n - 1);
+        if (!isfinite(mx) || !isfinite(my)) {
+          w = 1u << 18;
+        } else {
+          const double rx = rint(mx), ry = rint(my);
+          if (S.ana.ew_log) {  // combatant.py:146-150: (observer position, rounded fix)
+            const int fx = (int)fmin(fmax(rx, -32768.0), 32767.0), fy = (int)fmin(fmax(ry, -32768.0), 32767.0);
+            ana_record(S.ana.ew_log, S.ana.ew_count, S.ana.ew_cap, (uint32_t)(P.env_base + env - lane + s),
+                       (uint32_t)stp | (uint32_t)(me >= P.nb) << 16, c.pos_cur[me * PAD + s],
+                       (uint32_t)(uint16_t)fx | (uint32_t)(uint16_t)fy << 16);
+          }
+          if (rx >= 0.0 && rx < (double)P.G && ry >= 0.0 && ry < (double)P.G)
+            w = (uint32_t)(int)rx | (uint32_t)(int)ry << 8 | 1u << 16;
+        }
+      }
+      fixt[j * WAVE + s] = w;
+    };
+    // the previous round's last slot (rank nact-1, second slot)
+    double cm = 0.0, csx = 0.0, csy = 0.0;
+    uint32_t cp = 0;
+    int cz = 0;
     for (int r0 = 0; r0 < total; r0 += 2 * nact) {
-      const int g1 = min(r0 + rank, total - 1), g2 = min(r0 + nact + rank, total - 1);
-      int s1, s2;
-      uint32_t pi1, pj1, pi2, pj2;
-      unsigned long long d1, d2;
-      locate(g1, s1, pi1, pj1, d1);
-      locate(g2, s2, pi2, pj2, d2);
-      const int dx1 = pos_x(pj1) - pos_x(pi1), dy1 = pos_y(pj1) - pos_y(pi1);
-      const int dx2 = pos_x(pj2) - pos_x(pi2), dy2 = pos_y(pj2) - pos_y(pi2);
+      const int gA = r0 + 2 * rank, gB = gA + 1;
+      int sA, iA, jA, sB, iB, jB;
+      uint32_t nA, nB, piA, pjA, piB, pjB;
+      unsigned long long dA, dB;
+      locate(min(gA, total - 1), sA, iA, jA, nA, dA, piA, pjA);
+      locate(min(gB, total - 1), sB, iB, jB, nB, dB, piB, pjB);
+      const int dx1 = pos_x(pjA) - pos_x(piA), dy1 = pos_y(pjA) - pos_y(piA);
+      const int dx2 = pos_x(pjB) - pos_x(piB), dy2 = pos_y(pjB) - pos_y(piB);
       const BearPre b1 = bearing_pre(P, S, dx1, dy1), b2 = bearing_pre(P, S, dx2, dy2);
       double a1 = b1.v, a2 = b2.v;
       if (!(b1.tab && b2.tab)) {
         a1 = bearing_use(b1, dx1, dy1);
         a2 = bearing_use(b2, dx2, dy2);
       }
-      const double gg1 = draw(s1, d1), gg2 = draw(s2, d2);
+      const double gg1 = draw(sA, dA), gg2 = draw(sB, dB);
       // calculate_bearing (combatant.py:249-263)
       const double br1 = a1 + gg1 < 0 ? a1 + gg1 + 360.0 : a1 + gg1;
       const double br2 = a2 + gg2 < 0 ? a2 + gg2 + 360.0 : a2 + gg2;
-      const double m1 = tan_fd(br1 * DEG2RAD), m2 = tan_fd(br2 * DEG2RAD);
-      // owners take this round's slopes of their bearings, in order
-      const int rend = r0 + 2 * nact;
-      for (;;) {
-        const bool more = myn != 0 && myg < rend;
-        if (!__ballot(more)) break;
-        const int off = myg - r0;
-        const bool second = off >= nact;
-        const int src = more ? lor[(second ? off - nact : off) & (WAVE - 1)] : lane;
-        const double v1 = __shfl(m1, src), v2 = __shfl(m2, src);
-        if (more) {
-          const int t = __builtin_ctz(myn);
-          myn &= myn - 1;
-          myg++;
-          int dx, dy, j, k;
-          double x1, y1;
-          setup(t, dx, dy, j, x1, y1, k);
-          accum(j, second ? v2 : v1, x1, y1);
-        }
+      const double mA = tan_fd(br1 * DEG2RAD), mB = tan_fd(br2 * DEG2RAD);
+      // first / last bearing of its segment
+      const bool fA = !(nA & ((1u << iA) - 1u)), fB = !(nB & ((1u << iB) - 1u));
+      const bool lA = !(nA >> (iA + 1)), lB = !(nB >> (iB + 1));
+      // slot A's predecessor: the previous rank's slot B, or the carry
+      const double tm = __shfl(mB, prevl);
+      const uint32_t tp = (uint32_t)__shfl((int)piB, prevl);
+      const double pm = rank > 0 ? tm : cm;
+      const uint32_t pp = rank > 0 ? tp : cp;
+      double xA = 0.0, yA = 0.0, xB = 0.0, yB = 0.0;
+      const bool zA = !fA && pm - mA == 0.0, zB = !fB && mA - mB == 0.0;
+      if (!fA && !zA)
+        fix_pair(pm, mA, pos_x(pp), pos_y(pp), pos_x(piA), pos_y(piA), xA, yA);
+      if (!fB && !zB)
+        fix_pair(mA, mB, pos_x(piA), pos_y(piA), pos_x(piB), pos_y(piB), xB, yB);
+      // running sums (0.0 at a segment's first slot, then + each fix, left to
+      // right). Each pass carries the sums one lane hop further (a slot reads its
+      // predecessor's sum from the previous pass); a segment of at most NOWN slots
+      // is final after (NOWN - 1) / 2 + 1 passes
+      double sxA = 0.0, syA = 0.0, sxB = 0.0, syB = 0.0;
+      bool ZA = false, ZB = false;
+#pragma unroll
+      for (int pass = 0; pass < (NOWN - 1) / 2 + 1; pass++) {
+        const double qx = __shfl(sxB, prevl), qy = __shfl(syB, prevl);
+        const int qz = __shfl((int)ZB, prevl);
+        const double inx = rank > 0 ? qx : csx, iny = rank > 0 ? qy : csy;
+        const bool inz = (rank > 0 ? qz : cz) != 0;
+        sxA = fA ? 0.0 : inx + xA;
+        syA = fA ? 0.0 : iny + yA;
+        ZA = !fA && (inz || zA);
+        sxB = fB ? 0.0 : sxA + xB;
+        syB = fB ? 0.0 : syA + yB;
+        ZB = !fB && (ZA || zB);
+      }
+      int stA = 0, stB = 0;
+      if (S.ana.ew_log) {
+        stA = __shfl(X.step, sA);
+        stB = __shfl(X.step, sB);
+      }
+      if (gA < total && lA) finish(sA, jA, __builtin_popcount(nA), sxA, syA, ZA, stA);
+      if (gB < total && lB) finish(sB, jB, __builtin_popcount(nB), sxB, syB, ZB, stB);
+      // carry the last slot of the round
+      cm = __shfl(mB, lastl);
+      cp = (uint32_t)__shfl((int)piB, lastl);
+      csx = __shfl(sxB, lastl);
+      csy = __shfl(syB, lastl);
+      cz = __shfl((int)ZB, lastl);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < NOPP; j++) {
+      if (__builtin_popcount((need >> (j * NOWN)) & SEGM) < 2) continue;
+      const uint32_t w = fixt[j * WAVE + lane];
+      if (w & (1u << 17)) X.rng.err |= LNW_ERRF_ZERODIV;
+      else if (w & (1u << 18)) X.rng.err |= LNW_ERRF_NAN_ROUND;
+      else if (w & (1u << 16)) {
+        fxr[j] = (int)(w & 0xffu);
+        fyr[j] = (int)((w >> 8) & 0xffu);
+        fok |= 1u << j;
       }
     }
   } else
@@ -3000,7 +3082,8 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
     }
     if (bl > 0)
       fprintf(stderr, "[lnw prof] EW bearings (contact variant): %.0f evaluated, wave max summed %.0f, "
-                      "active lanes %.0f; balanced/actual %.3f\n", bs, bm, bl, bs / 64.0 / bm);
+                      "active lanes %.0f; balanced/actual %.3f\n",
+              bs, bm, bl, bs / 64.0 / bm);
   }
   if (nq)
     fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us\n",

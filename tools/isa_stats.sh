@@ -3,7 +3,7 @@
 cd "$(dirname "$0")/.." || exit 1
 C=littoral-naval-warfare-marl_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-gpu-flush-denormals-to-zero \
-  -Iinclude -I$C --cuda-device-only -c $C/lnw_kernels.hip -o /tmp/lnw_isa.o 2>/dev/null || exit 1
+  -Iinclude -I${SRC:-$C} --cuda-device-only -c ${SRC:-$C}/lnw_kernels.hip -o /tmp/lnw_isa.o 2>/dev/null || exit 1
 /opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input=/tmp/lnw_isa.o \
   --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=/tmp/lnw_isa_dev.o || exit 1
 /opt/rocm/lib/llvm/bin/llvm-objdump -d --mcpu=gfx950 /tmp/lnw_isa_dev.o > /tmp/lnw_isa.txt
