@@ -335,20 +335,29 @@ def test_episode_gpu_tape_march_astar(name, grids):
     _cmp_episode(name, grids, los_mode=1, move_mode=1)
 
 
+@pytest.mark.parametrize("contact", [False, True])
 @pytest.mark.parametrize("name", ["ep_ana_melee.npz", "ep_ana_melee_red.npz",
                                   "ep_ana_split_observe.npz"])
-def test_analytics_replay(name, grids):
+def test_analytics_replay(name, contact, grids):
     """Analytics side channels (lnw_set_analytics) against the reference's
     heatmap / coldmap / launch_sites / engagements / blue_ew / red_ew recorded
-    over the same tape-mode episodes (make_golden.py make_analytics_episodes)."""
+    over the same tape-mode episodes (make_golden.py make_analytics_episodes),
+    through both step-kernel variants (the contact variant's pooled bearings
+    record the EW fixes from the lane that finishes them)."""
     from _gpu_replay import replay_gpu
     fx = load_fixture(name)
     n_steps = np.array([em["n_steps"] for em in episode_meta(fx)["episodes"]])
     g = None
-    for kind, info, g, res in replay_gpu(fx, grids):
+    counting = False
+    for kind, info, g, res in replay_gpu(fx, grids, contact=contact):
         if kind == "reset":
             g.enable_analytics(eng_cap=4096, ew_cap=4096)
+            if contact and not counting:
+                g.count_work(True)
+                counting = True
     torch.cuda.synchronize()
+    if contact and "melee" in name:  # the pooled path ran
+        assert g.work_counts()["pooled_bearings"] > 0
     an = g.analytics()
     assert an["engagements_total"] <= 4096 and an["ew_total"] <= 4096
     np.testing.assert_array_equal(an["heatmap"].cpu().numpy(), fx["ana_heat"].sum(0))
