@@ -300,6 +300,23 @@ struct Rng {
     block(o);
     return u53(o[0], o[1]);
   }
+  // two consecutive uniform draws (fire_missile's detection and hit draws);
+  // Philox: both counter blocks evaluated side by side
+  __device__ __forceinline__ void uniform2(double &u1, double &u2) {
+    if (mode == 1) {
+      u1 = tnext();
+      u2 = tnext();
+      return;
+    }
+    uint32_t o1[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), g0, g1};
+    const unsigned long long c2 = ctr + 1;
+    uint32_t o2[4] = {(uint32_t)c2, (uint32_t)(c2 >> 32), g0, g1};
+    philox10(o1, k0, k1);
+    philox10(o2, k0, k1);
+    ctr += 2;
+    u1 = u53(o1[0], o1[1]);
+    u2 = u53(o2[0], o2[1]);
+  }
   __device__ double gauss() {
     if (mode == 1) return tnext();
     uint32_t o[4];

@@ -1470,7 +1470,8 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
     int miss = COLB(c.miss_cur, a);
     if (miss == 0) return false;
     int mk = COLB(c.mkind, a);
-    double u1 = X.rng.uniform();
+    double u1, u2;  // the detection draw, then the hit draw (combatant.py:612, 630)
+    X.rng.uniform2(u1, u2);
     bool detected = !(u1 < (COLW(c.radar_cur, t) == 1 ? P.det_q[0] : P.det_q[1]));
     int hp = detected ? 0 : 1;
     double num;
@@ -1492,7 +1493,6 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
     n = (int)num;
     COLB(c.miss_cur, a) = (uint8_t)(miss - n);
     COLB(c.mkind, a) = (uint8_t)kind_promote(mk, kn);
-    double u2 = X.rng.uniform();
     if (n < 0 || n > 8) { X.rng.err |= LNW_ERRF_MISSILES; n = n < 0 ? 0 : 8; }
     if (kn == K_F32)
       hit = (float)u2 < hit_sel(P.hit32, hp, n);
@@ -2603,8 +2603,10 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
         int tn = (int)COLW(c.tcnt, a);
         if (engage && tn > 0) {
           const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
+          uint16_t nx = tl[0];  // the next target's load is in flight while one fires
           for (int q = 0; q < tn; q++) {
-            uint16_t tg = tl[(size_t)q * E];
+            const uint16_t tg = nx;
+            if (q + 1 < tn) nx = tl[(size_t)(q + 1) * E];
             if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
           }
         }
@@ -3064,6 +3066,21 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
     for (int w = 0; w < nwg; w++) {
       const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
       if (r[2] > r[1]) sv.push_back((double)(r[2] - r[1]) * 0.01);
+    }
+    {  // the slowest workgroup's parts (slots 16..23)
+      int wm = -1;
+      double best = -1;
+      for (int w = 0; w < nwg; w++) {
+        const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+        if (r[2] > r[1] && (double)(r[2] - r[1]) > best) { best = (double)(r[2] - r[1]); wm = w; }
+      }
+      if (wm >= 0) {
+        const unsigned long long *r = &t[(size_t)wm * PROF_SLOTS];
+        fprintf(stderr, "[lnw prof] slowest workgroup %d: S %.1f us = take_action %.1f, LOS prefetch %.1f, get_obs %.1f "
+                        "(walk %.1f, observed %.1f, bearings %.1f, fix targets %.1f), reward %.1f\n",
+                wm, best * 0.01, r[16] * 0.01, r[17] * 0.01, r[18] * 0.01, r[20] * 0.01, r[21] * 0.01,
+                r[22] * 0.01, r[23] * 0.01, r[19] * 0.01);
+      }
     }
     std::sort(sv.begin(), sv.end());
     if (!sv.empty())
