@@ -30,6 +30,7 @@ using namespace lnw;
 // native 4 x f32 vector: arrays of it stay in VGPRs (HIP's union-based float4
 // defeats SROA and lands such arrays in scratch)
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -781,7 +782,7 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
 template <int NOWN, int NOPP, bool CW>
 __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_n,
                                     uint32_t firstbit, uint32_t bearm,
-                                    const uint32_t (&pp)[NOPP]) {
+                                    const uint32_t (&pp)[NOPP], uint32_t oal = 0) {
   static_assert(NOWN < 9, "np.mean pairwise summation starts at 8 terms");
   const KParams &P = X.P;
   const KState &S = X.S;
@@ -804,7 +805,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
   // observed positions (combatant.py:152-154)
   if constexpr (CW) {  // one per cell class, in the order of each class's first detecting pair
     for (uint32_t fb = firstbit; fb; fb &= fb - 1) {
-      const uint32_t pk = rsel(pp, __builtin_ctz(fb) % NOPP);
+      const uint32_t pk = COLW(c.pos_cur, opp0 + __builtin_ctz(fb) % NOPP);
       tl[(size_t)tn * E] = (uint16_t)(pos_x(pk) | (pos_y(pk) << 8));
       tn++;
     }
@@ -846,9 +847,10 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
       atomicAdd(&S.prof[(size_t)blockIdx.x * PROF_SLOTS + 26], (unsigned long long)__popcll(m));
     }
   }
-  int fxr[NOPP], fyr[NOPP];
-#pragma unroll
-  for (int j = 0; j < NOPP; j++) fxr[j] = fyr[j] = 0;
+  // opponent j's rounded fix, x | y << 8, in bits 16j..16j+15 (a register
+  // array indexed by a runtime j would live in scratch)
+  static_assert(NOPP <= 4, "fix cells packed 16 bits per opponent");
+  uint64_t fixw = 0;
   uint32_t fok = 0;  // opponent j has a rounded fix inside the grid
   int curj = -1, cnt = 0;
   bool zero = false;
@@ -867,11 +869,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
                  (uint32_t)(uint16_t)fx | (uint32_t)(uint16_t)fy << 16);
     }
     if (!(rx >= 0.0 && rx < (double)P.G && ry >= 0.0 && ry < (double)P.G)) return;
-#pragma unroll
-    for (int j = 0; j < NOPP; j++) {
-      fxr[j] = curj == j ? (int)rx : fxr[j];
-      fyr[j] = curj == j ? (int)ry : fyr[j];
-    }
+    fixw |= (uint64_t)((uint32_t)(int)rx | (uint32_t)(int)ry << 8) << (16 * curj);
     fok |= 1u << curj;
   };
   if constexpr (CW) {
@@ -1090,8 +1088,7 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
       if (w & (1u << 17)) X.rng.err |= LNW_ERRF_ZERODIV;
       else if (w & (1u << 18)) X.rng.err |= LNW_ERRF_NAN_ROUND;
       else if (w & (1u << 16)) {
-        fxr[j] = (int)(w & 0xffu);
-        fyr[j] = (int)((w >> 8) & 0xffu);
+        fixw |= (uint64_t)(w & 0xffffu) << (16 * j);
         fok |= 1u << j;
       }
     }
@@ -1163,11 +1160,13 @@ __device__ inline void finish_obs_t(Ctx &X, int me, int own0, int opp0, int obs_
     if ((done >> jj) & 1u) continue;
     done |= 1u << jj;
     if (!((fok >> jj) & 1u)) continue;
-    const int fxi = rsel(fxr, jj), fyi = rsel(fyr, jj);
+    const uint32_t fw = (uint32_t)(fixw >> (16 * jj));
+    const int fxi = (int)(fw & 0xffu), fyi = (int)((fw >> 8) & 0xffu);
 #pragma unroll
     for (int j = 0; j < NOPP; j++) {
-      if (!COLB(c.alive0, opp0 + j)) continue;
-      const uint32_t pj = COLW(c.pos_cur, opp0 + j);
+      // (contact variant: the opponents' cells and alive bits from the walk's registers)
+      if (CW ? !((oal >> j) & 1u) : !COLB(c.alive0, opp0 + j)) continue;
+      const uint32_t pj = CW ? pp[j] : COLW(c.pos_cur, opp0 + j);
       const int ddx = pos_x(pj) - fxi, ddy = pos_y(pj) - fyi;
       if (ddx * ddx + ddy * ddy < 4) {
         tl[(size_t)tn * E] = (uint16_t)(fxi | (fyi << 8));
@@ -1326,7 +1325,7 @@ __device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp
     bearm |= ewm & (colj << j) & (f ? f - 1u : 0xffffffffu);
   }
   prof_acc(X.S, 20, tw);
-  finish_obs_t<NOWN, NOPP, true>(X, me, own0, opp0, 0, firstbit, bearm, pp);
+  finish_obs_t<NOWN, NOPP, true>(X, me, own0, opp0, 0, firstbit, bearm, pp, amask >> NOWN);
 }
 
 // get_obs for compile-time ship counts: CW selects the contact variant
@@ -1420,11 +1419,19 @@ __device__ inline void los_prefetch_t(Ctx &X) {
     while (marchm) {  // outside the table window (very long sensor ranges)
       const int u = __builtin_ctz(marchm);
       marchm &= marchm - 1;
-      int x1, y1, x2, y2;
-      bool need;
-      ray(r0 + u, x1, y1, x2, y2, need);
-      const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR);
-      bits[s] |= (uint64_t)los_march_c(X.S, X.mask, P.W16, x1, y1, x2, y2) << (2 * q);
+      // the ray's cells again from the LDS columns: a runtime index into the
+      // register arrays above would put them in scratch for the whole function
+      const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR), v = q & 1, p = q >> 1;
+      const int o = s == 0 ? p / NR : NB + p / NB, d = s == 0 ? NB + p % NR : p % NB;
+      const uint32_t pn = COLW(c.pos_new, o);
+      const uint32_t po = v && (pn & 0x80000000u) ? (pn & 0x7fffffffu) : COLW(c.pos_cur, o);
+      uint32_t pd = COLW(c.pos_cur, d);
+      if (s == 1) {  // red -> blue rays end at the blue ship's final cell
+        const uint32_t qn = COLW(c.pos_new, d);
+        if (qn & 0x80000000u) pd = qn & 0x7fffffffu;
+      }
+      bits[s] |= (uint64_t)los_march_c(X.S, X.mask, P.W16, pos_x(po), pos_y(po), pos_x(pd), pos_y(pd))
+                 << (2 * q);
     }
   }
   X.lpre[0] = bits[0];
@@ -1556,7 +1563,7 @@ __device__ __forceinline__ double reward_core(const KParams &P, const KState &S,
     int dx = x - P.lz_x, dy = y - P.lz_y;
     double dl = sqrt((double)(dx * dx + dy * dy));
     if (dl > 0) {
-      double cur = S.dist_lz[ai];
+      double cur = (P.dbg_skip & 2097152) ? 1e9 : S.dist_lz[ai];  // (bit 21: diagnostics)
       if (dl < cur) { r += 1.0; S.dist_lz[ai] = dl; }
       else r -= 1.0;
     } else {
@@ -2080,11 +2087,11 @@ __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, c
 template <int NW>
 __device__ __forceinline__ void stage_mask(const KParams &P, const KState &S, uint32_t *dst) {
   const int nw = P.G * P.W16, n4 = nw >> 2;
-  const uint4 *src4 = (const uint4 *)S.mask2;
-  uint4 *dst4 = (uint4 *)dst;
+  const u32x4 *src4 = (const u32x4 *)S.mask2;
+  u32x4 *dst4 = (u32x4 *)dst;
   constexpr int U = 4;
   for (int i0 = threadIdx.x; i0 < n4; i0 += U * NW * WAVE) {
-    uint4 v[U];
+    u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int i = i0 + u * NW * WAVE;
@@ -2601,13 +2608,33 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
           thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
         engage = thr_v > 0.0;
         int tn = (int)COLW(c.tcnt, a);
-        if (engage && tn > 0) {
+        if (engage && tn > 0 && !(P.dbg_skip & 65536)) {  // (bit 16: diagnostics, no fire)
           const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
-          uint16_t nx = tl[0];  // the next target's load is in flight while one fires
-          for (int q = 0; q < tn; q++) {
-            const uint16_t tg = nx;
-            if (q + 1 < tn) nx = tl[(size_t)(q + 1) * E];
-            if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+          if constexpr (CW) {
+            // contact variant: the list read 8 entries at a time, the loads of a
+            // chunk in flight together (packed in a register pair: a runtime index
+            // into a register array would put it in scratch)
+            for (int q0 = 0; q0 < tn; q0 += 8) {
+              uint64_t pk0 = 0, pk1 = 0;
+#pragma unroll
+              for (int u = 0; u < 8; u++) {
+                const uint64_t v = q0 + u < tn ? (uint64_t)tl[(size_t)(q0 + u) * E] : 0ull;
+                if (u < 4) pk0 |= v << (16 * u);
+                else pk1 |= v << (16 * (u - 4));
+              }
+              const int nq = tn - q0 < 8 ? tn - q0 : 8;
+              for (int u = 0; u < nq; u++) {
+                const uint16_t tg = (uint16_t)((u < 4 ? pk0 : pk1) >> (16 * (u & 3)));
+                if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+              }
+            }
+          } else {
+            uint16_t nx = tl[0];  // the next target's load is in flight while one fires
+            for (int q = 0; q < tn; q++) {
+              const uint16_t tg = nx;
+              if (q + 1 < tn) nx = tl[(size_t)(q + 1) * E];
+              if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+            }
           }
         }
         if (side) ev[6] += destroyed; else ev[5] += destroyed;
@@ -3290,7 +3317,10 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     bool atan_lds;
     const size_t gneed = (size_t)group_lds_bytes((int)step_lds_bytes(h), h->nb * h->nr, atan_lds) + 1024;
-    h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX;  // else runtime sizes stay on step_kernel<0, 0>
+    // (else runtime sizes stay on step_kernel<0, 0>; the pair masks need the
+    // observed-list region: 1v1 is too small)
+    h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX &&
+                    h->nmax * (PAD * 4 + 2 * PADB) >= group_mask_bytes(h->nb * h->nr);
     // the limit is per kernel function, shared by every handle of the process:
     // set to the CU's whole LDS once, so a smaller handle never lowers it under
     // a larger one's launch (the launch's own size sets the occupancy)

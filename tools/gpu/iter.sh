@@ -8,6 +8,6 @@ timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu-baseline > gp
 python -c "import json; d=json.load(open('gpurun_out/bench.json')); print('REF', d['value']/1e6, 'M', d['roofline']['kernel_ms_mean']*1e3, 'us')"
 timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --spawns melee > gpurun_out/bm.json 2> gpurun_out/bm.err || exit 4
 python -c "import json; d=json.load(open('gpurun_out/bm.json')); print('MELEE', d['value']/1e6, 'M', d['roofline']['kernel_ms_mean']*1e3, 'us')"
-LNW_PROF=1 timeout -k 10 300 python bench.py --steps 3 --warmup 5 --no-cpu-baseline --spawns melee > gpurun_out/pm.json 2> gpurun_out/pm.err || exit 5
+LNW_PROF=1 timeout -k 10 300 python bench.py --steps 3 --warmup 5 --no-cpu-baseline --no-secondary --spawns melee > gpurun_out/pm.json 2> gpurun_out/pm.err || exit 5
 grep "lnw prof" gpurun_out/pm.err | tail -2
 grep "lnw prof" gpurun_out/pm.err | tail -1

@@ -42,6 +42,11 @@ int main() {
   per_call_us([&] { k_big<<<1024, 128, 0, st>>>(b, nullptr); }, n);
   printf("700-byte args + 39 KB dynamic LDS:\n");
   per_call_us([&] { k_big<<<1024, 128, 39 * 1024, st>>>(b, nullptr); }, n);
+  (void)hipFuncSetAttribute((const void *)k_big, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+  printf("700-byte args, 512 x 256 threads + 78 KB LDS:\n");
+  per_call_us([&] { k_big<<<512, 256, 78 * 1024, st>>>(b, nullptr); }, n);
+  printf("700-byte args, 256 x 512 threads + 156 KB LDS:\n");
+  per_call_us([&] { k_big<<<256, 512, 156 * 1024, st>>>(b, nullptr); }, n);
   printf("scratch kernel:\n");
   per_call_us([&] { k_scratch<<<1024, 128, 0, st>>>(nullptr, 3); }, n);
   // graph of 100 launches
