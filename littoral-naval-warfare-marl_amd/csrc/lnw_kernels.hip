@@ -2486,7 +2486,14 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // after M wave 1 turns to emission and wave 0 runs S
   constexpr int NW = ST && EPW == WAVE ? 2 : 1;
   if (NW == 1 && wid == 1) return;
-  if (wid == 0) prof_stamp(S, 0);
+  if (wid == 0) {
+    prof_stamp(S, 0);
+    // XCC id (hwreg 20, bits 3:0) and HW_ID (hwreg 4: CU, SH, SE) of this workgroup
+    prof_put(S, 30, (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20));
+    prof_put(S, 31, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  } else if (wid == 1) {
+    prof_put(S, 29, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  }
 
   stage_mask<NW>(P, S, c.mask);
   const uint32_t *mask = c.mask;
@@ -3128,6 +3135,87 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
       fprintf(stderr, "[lnw prof] EW bearings (contact variant): %.0f evaluated, wave max summed %.0f, "
                       "active lanes %.0f; balanced/actual %.3f\n",
               bs, bm, bl, bs / 64.0 / bm);
+  }
+  {  // grid timeline: workgroup start (slot 0), stream / phase S start (slot 1),
+     // wave-1 end (slot 5), each as p10 / p50 / p90 / max after the first start
+    const int slots[3] = {0, 1, 5};
+    const char *names[3] = {"start", "S/stream start", "wave-1 end"};
+    for (int k = 0; k < 3; k++) {
+      std::vector<double> sv;
+      for (int w = 0; w < nwg; w++) {
+        const unsigned long long v = t[(size_t)w * PROF_SLOTS + slots[k]];
+        if (v >= t0) sv.push_back((double)(v - t0) * us);
+      }
+      std::sort(sv.begin(), sv.end());
+      if (!sv.empty())
+        fprintf(stderr, "[lnw prof] timeline %s: p10 %.2f, p50 %.2f, p90 %.2f, max %.2f us\n", names[k],
+                sv[sv.size() / 10], sv[sv.size() / 2], sv[sv.size() * 9 / 10], sv.back());
+    }
+  }
+  {  // wave-1 end (slot 5) per XCC: count, mean, max after the first start
+    double se[16] = {0}, mx[16] = {0};
+    int nx[16] = {0};
+    for (int w = 0; w < nwg; w++) {
+      const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+      if (!r[5] || r[5] < t0) continue;
+      const int x = (int)(r[30] & 15);
+      const double e = (double)(r[5] - t0) * us;
+      se[x] += e; nx[x]++;
+      if (e > mx[x]) mx[x] = e;
+    }
+    {  // per CU (XCC, SE, SH, CU from HW_ID bits 15:8): spread of CU means vs within-CU spread
+      std::vector<std::pair<int, double>> v;
+      for (int w = 0; w < nwg; w++) {
+        const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+        if (!r[5] || r[5] < t0) continue;
+        v.push_back({(int)((r[30] & 15) << 8 | ((r[31] >> 8) & 0xff)), (double)(r[5] - t0) * us});
+      }
+      std::sort(v.begin(), v.end());
+      std::vector<double> means, spans;
+      for (size_t i = 0; i < v.size();) {
+        size_t j = i;
+        double sm = 0, lo = 1e30, hi = -1e30;
+        while (j < v.size() && v[j].first == v[i].first) { sm += v[j].second; lo = std::min(lo, v[j].second); hi = std::max(hi, v[j].second); j++; }
+        means.push_back(sm / (double)(j - i));
+        spans.push_back(hi - lo);
+        i = j;
+      }
+      std::sort(means.begin(), means.end());
+      std::sort(spans.begin(), spans.end());
+      if (!means.empty())
+        fprintf(stderr, "[lnw prof] CUs %zu: CU-mean wave-1 end p10 %.1f p50 %.1f p90 %.1f max %.1f; within-CU span p50 %.1f p90 %.1f max %.1f us\n",
+                means.size(), means[means.size() / 10], means[means.size() / 2], means[means.size() * 9 / 10], means.back(),
+                spans[spans.size() / 2], spans[spans.size() * 9 / 10], spans.back());
+    }
+    {  // SIMD placement: wave 0 (phase S) sharing its SIMD with another workgroup's wave 0
+      std::vector<int> key(nwg);
+      for (int w = 0; w < nwg; w++) {
+        const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+        key[w] = (int)((r[30] & 15) << 12 | ((r[31] >> 8) & 0xff) << 4 | ((r[31] >> 4) & 3));
+      }
+      std::vector<int> sk = key;
+      std::sort(sk.begin(), sk.end());
+      double e0[2] = {0, 0}, m0[2] = {0, 0};
+      int n0[2] = {0, 0}, same = 0;
+      for (int w = 0; w < nwg; w++) {
+        const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+        const int cnt = (int)(std::upper_bound(sk.begin(), sk.end(), key[w]) - std::lower_bound(sk.begin(), sk.end(), key[w]));
+        const int k = cnt > 1 ? 1 : 0;
+        if (r[3] < t0) continue;
+        const double e = (double)(r[3] - t0) * us;
+        e0[k] += e; n0[k]++;
+        if (e > m0[k]) m0[k] = e;
+        same += ((r[31] >> 4) & 3) == ((r[29] >> 4) & 3);
+      }
+      fprintf(stderr, "[lnw prof] wave-0 SIMD: alone %d (end mean %.1f max %.1f us), shared %d (mean %.1f max %.1f us); "
+                      "waves 0/1 on one SIMD in %d workgroups\n",
+              n0[0], n0[0] ? e0[0] / n0[0] : 0.0, m0[0], n0[1], n0[1] ? e0[1] / n0[1] : 0.0, m0[1], same);
+    }
+    fprintf(stderr, "[lnw prof] wave-1 end by XCC (n/mean/max us):");
+    for (int x = 0; x < 16; x++)
+      if (nx[x]) fprintf(stderr, " %d:%d/%.1f/%.1f", x, nx[x], se[x] / nx[x], mx[x]);
+    fprintf(stderr, "; block%%8==xcc for %d of %d\n",
+            [&] { int k = 0; for (int w = 0; w < nwg; w++) k += (int)(t[(size_t)w * PROF_SLOTS + 30] & 15) == (w & 7); return k; }(), nwg);
   }
   if (nq)
     fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us\n",
