@@ -197,17 +197,19 @@ def run_workload(E, env_base, spawns, los_mode, move_mode, steps, warmup, cfg=No
 def measured_traffic(args, E):
     """HBM bytes per launch from rocprofv3 PMC counters (2 x FETCH_SIZE +
     WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), as recorded in
-    profiles/traffic.json by tools/gpu/traffic.sh together with the SHA-256 of
-    the liblnw.so it measured. Reported only if this run loads that same
-    library; otherwise null."""
-    import hashlib
+    profiles/traffic.json by tools/gpu/prof.sh together with the SHA-256 of
+    the sources and flags of the liblnw.so it measured (lnw.build.source_digest).
+    Reported only if this run's library is built from those same sources (and
+    is the in-tree build); otherwise null."""
     from lnw import _abi
+    from lnw.build import DEPS, OUT, source_digest
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         tj = json.load(open(tf))
-        with open(_abi.LIB_PATH, "rb") as f:
-            sha = hashlib.sha256(f.read()).hexdigest()
-        if tj.get("lib_sha256") != sha:
+        lib = os.path.realpath(os.environ.get("LNW_LIB", _abi.LIB_PATH))
+        if lib != os.path.realpath(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in DEPS):
+            return None  # another library, or an in-tree build older than its sources
+        if tj.get("src_sha256") != source_digest():
             return None
         wl = "config4" if args.workload == "config4" else args.spawns
         return tj.get("launch_bytes", {}).get(f"{wl}_e{E}_los{args.los_mode}_mv{args.move_mode}")

@@ -32,6 +32,19 @@ def flags(arch="gfx950"):
             "-fno-gpu-flush-denormals-to-zero", "-fPIC", "-shared", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
+def source_digest():
+    """SHA-256 over the compiler flags and every source liblnw.so is built
+    from: identifies the kernel code a measurement was taken on (hipcc's output
+    bytes differ between otherwise identical builds)."""
+    import hashlib
+    h = hashlib.sha256(" ".join(flags()).encode())
+    for d in DEPS:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def build(force=False, verbose=False, out=OUT, defines=()):
     """liblnw.so (or a diagnostics variant at `out` built with -D`defines`)."""
     if not force and os.path.exists(out):

@@ -87,13 +87,15 @@ def main():
                       f"{alg / 1e6:.2f} MB ({B} B/env-step x {E}); ratio {traffic / alg:.3f}"]
         tf = os.path.join(PROF, "traffic.json")
         tj = json.load(open(tf)) if os.path.exists(tf) else {}
-        with open(os.path.join(ROOT, "littoral-naval-warfare-marl_amd", "lnw", "liblnw.so"), "rb") as f:
-            sha = hashlib.sha256(f.read()).hexdigest()
-        if tj.get("lib_sha256") != sha:
-            tj = {"lib_sha256": sha, "launch_bytes": {}}
+        sys.path.insert(0, os.path.join(ROOT, "littoral-naval-warfare-marl_amd"))
+        from lnw.build import source_digest
+        sha = source_digest()
+        if tj.get("src_sha256") != sha:
+            tj = {"src_sha256": sha, "launch_bytes": {}}
         tj.setdefault("launch_bytes", {})[key] = traffic
         tj["_note"] = ("HBM bytes per step_kernel launch = 2*FETCH_SIZE + WRITE_SIZE from rocprofv3 PMC, "
-                       "for the liblnw.so with this SHA-256 (tools/gpu/prof.sh, profiles/*_rocprof.md)")
+                       "for the liblnw.so built from the sources and flags with this SHA-256 "
+                       "(lnw.build.source_digest; tools/gpu/prof.sh, profiles/*_rocprof.md)")
         json.dump(tj, open(tf, "w"), indent=1)
     if "SQ_WAVES" in pmc and "SQ_INSTS_VALU" in pmc:
         w = pmc["SQ_WAVES"]
