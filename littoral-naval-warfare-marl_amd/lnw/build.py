@@ -37,7 +37,8 @@ def source_digest():
     from: identifies the kernel code a measurement was taken on (hipcc's output
     bytes differ between otherwise identical builds)."""
     import hashlib
-    h = hashlib.sha256(" ".join(flags()).encode())
+    # flags without the include paths (the tree's location differs between machines)
+    h = hashlib.sha256(" ".join(f for f in flags() if not f.startswith("-I")).encode())
     for d in DEPS:
         h.update(os.path.basename(d).encode())
         with open(d, "rb") as f:
