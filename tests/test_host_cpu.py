@@ -53,3 +53,45 @@ def test_packaged_grid_is_the_reference_grid():
     g = np.load(os.path.join(ROOT, "tests", "golden", "grids.npz"))
     assert np.array_equal(default_grid(100), g["grid100"])
     assert np.array_equal(default_grid(200), g["grid200"])
+
+
+def test_measured_traffic_keyed_to_sources(tmp_path, monkeypatch):
+    """bench.py reports roofline.traffic only for the in-tree library built from
+    the sources profiles/traffic.json was measured on (lnw.build.source_digest):
+    a different digest, or another library through LNW_LIB, gives null."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from lnw import build
+
+    class Args:
+        workload, spawns, los_mode, move_mode = "reference", "reference", 0, 0
+
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.delenv("LNW_LIB", raising=False)
+    key = "reference_e64_los0_mv0"
+    tj = {"src_sha256": build.source_digest(), "launch_bytes": {key: 123.0}}
+    (prof / "traffic.json").write_text(json.dumps(tj))
+    fresh = os.path.exists(build.OUT) and all(
+        os.path.getmtime(d) <= os.path.getmtime(build.OUT) for d in build.DEPS)
+    assert bench.measured_traffic(Args, 64) == (123.0 if fresh else None)
+    assert bench.measured_traffic(Args, 128) is None  # no record for this workload
+    monkeypatch.setenv("LNW_LIB", str(tmp_path / "other.so"))
+    assert bench.measured_traffic(Args, 64) is None
+    monkeypatch.delenv("LNW_LIB")
+    tj["src_sha256"] = "0" * 64
+    (prof / "traffic.json").write_text(json.dumps(tj))
+    assert bench.measured_traffic(Args, 64) is None
+
+
+def test_source_digest_ignores_tree_location(monkeypatch):
+    """The digest hashes flags without include paths and file contents by
+    basename, so the GPU box (another tree path) computes the same value."""
+    from lnw import build
+    d = build.source_digest()
+    assert len(d) == 64
+    monkeypatch.setattr(build, "INCLUDE", "/elsewhere/include")
+    monkeypatch.setattr(build, "CSRC", "/elsewhere/csrc")
+    assert "-I/elsewhere/include" in build.flags()
+    assert build.source_digest() == d
