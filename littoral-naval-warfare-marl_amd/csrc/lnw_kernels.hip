@@ -2150,10 +2150,12 @@ __device__ inline void load_state(const KParams &P, const KState &S, Cols &c, in
 // reads 64 consecutive action rows (one coalesced 1 KB load) and all passes'
 // loads of one batch are issued before any is used.
 // ---------------------------------------------------------------------------
-template <int DT, int MAXP>
+// PRE (float32 rows, one batch): the rows were loaded before phase L's barrier
+// (preload_rows_f32) and arrive in vpre.
+template <int DT, int MAXP, bool PRE = false>
 __device__ __forceinline__ bool move_batch_t(const KParams &P, const KState &S, Cols &c, const void *actions,
                              const uint8_t *row_kind, const uint32_t *mask, int env0, int nenv,
-                             int A, int p0, int np) {
+                             int A, int p0, int np, const f32x4 (&vpre)[MAXP] = {}) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int npair = nenv * A;
   f32x4 vf[DT == LNW_ACT_F32 ? MAXP : 1];
@@ -2166,7 +2168,7 @@ __device__ __forceinline__ bool move_batch_t(const KParams &P, const KState &S, 
     int q = (p0 + k) * WAVE + lane;
     q = q < npair ? q : 0;  // absent pairs re-read pair 0 (ignored)
     const size_t row = ((size_t)env0 * A + q) * 4;
-    if constexpr (DT == LNW_ACT_F32) vf[k] = *(const f32x4 *)((const float *)actions + row);
+    if constexpr (DT == LNW_ACT_F32) vf[k] = PRE ? vpre[k] : *(const f32x4 *)((const float *)actions + row);
     else if constexpr (DT == LNW_ACT_I32) vi[k] = *(const int4 *)((const int32_t *)actions + row);
     else {
       const double2 *da = (const double2 *)((const double *)actions + row);
@@ -2291,6 +2293,37 @@ __device__ __forceinline__ void move_astar_pass(const KParams &P, const KState &
                                    pos_y(t2), c.open + lane, EPW);
     c.pos_new[a * PAD + e] = feas ? (t2 | 0x80000000u) : p;
   }
+}
+
+// Compile-time team sizes, float32 rows: a wave's share of the pair passes is at
+// most 4 (A <= 8, <= 64 envs), one batch. Its rows are loaded at launch, before
+// phase L's barrier, so their HBM round trip overlaps the state loads instead of
+// following them (move_phase_pre consumes them after the barrier).
+template <int NW, int MAXP>
+__device__ __forceinline__ void preload_rows_f32(const void *actions, int env0, int nenv, int A, int wid,
+                                                 f32x4 (&v)[MAXP]) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int npair = nenv * A;
+  const int npass = (npair + WAVE - 1) / WAVE;
+  const int share = (npass + NW - 1) / NW;
+  const int pbeg = wid * share, np = (pbeg + share < npass ? pbeg + share : npass) - pbeg;
+#pragma unroll
+  for (int k = 0; k < MAXP; k++) {
+    if (k >= np) break;
+    int q = (pbeg + k) * WAVE + lane;
+    q = q < npair ? q : 0;  // absent pairs re-read pair 0 (ignored)
+    v[k] = *(const f32x4 *)((const float *)actions + ((size_t)env0 * A + q) * 4);
+  }
+}
+template <int NW, int MAXP>
+__device__ __forceinline__ bool move_phase_pre(const KParams &P, const KState &S, Cols &c, const void *actions,
+                                               const uint8_t *row_kind, const uint32_t *mask, int env0,
+                                               int nenv, int A, int wid, const f32x4 (&v)[MAXP]) {
+  const int npass = (nenv * A + WAVE - 1) / WAVE;
+  const int share = (npass + NW - 1) / NW;
+  const int pbeg = wid * share, np = (pbeg + share < npass ? pbeg + share : npass) - pbeg;
+  if (np <= 0) return false;
+  return move_batch_t<LNW_ACT_F32, MAXP, true>(P, S, c, actions, row_kind, mask, env0, nenv, A, pbeg, np, v);
 }
 
 // The NW waves of the workgroup take contiguous halves of the passes.
@@ -2486,6 +2519,13 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // after M wave 1 turns to emission and wave 0 runs S
   constexpr int NW = ST && EPW == WAVE ? 2 : 1;
   if (NW == 1 && wid == 1) return;
+  // templated team sizes, float32 rows: this wave's action rows in flight across phase L
+  // (LNW_DEBUG_SKIP bit 23: loaded in phase M instead)
+  constexpr int MAXPRE = 4;  // passes per wave: A <= 8 ships x <= 64 envs over two waves
+  const int dt = P.act_dtype;
+  const bool pre = ST && NW == 2 && dt == LNW_ACT_F32 && !(P.dbg_skip & 4) && !(P.dbg_skip & 8388608);
+  f32x4 vpre[MAXPRE];
+  if (pre) preload_rows_f32<NW, MAXPRE>(actions, env0, nenv, A, wid, vpre);
   if (wid == 0) {
     prof_stamp(S, 0);
     // XCC id (hwreg 20, bits 3:0) and HW_ID (hwreg 4: CU, SH, SE) of this workgroup
@@ -2510,10 +2550,11 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // ---- phase M: movement feasibility for every agent of this env --------
   // M1: load each action row once (a0/a1 kept in LDS for phase S) and compute
   //     the move target; M2: feasibility lookups (independent across agents).
-  const int dt = P.act_dtype;
   bool pend = false;
   if (!(P.dbg_skip & 4)) {
-    if (dt == LNW_ACT_F32)
+    if (pre)
+      pend = move_phase_pre<NW, MAXPRE>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid, vpre);
+    else if (dt == LNW_ACT_F32)
       pend = move_phase<LNW_ACT_F32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
     else if (dt == LNW_ACT_F64)
       pend = move_phase<LNW_ACT_F64, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
