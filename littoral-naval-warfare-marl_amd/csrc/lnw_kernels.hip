@@ -3014,6 +3014,7 @@ struct lnw_handle {
   uint8_t *d_grid = nullptr;
   float *d_gridf = nullptr, *d_winf = nullptr, *d_dummy = nullptr;
   unsigned long long *d_prof = nullptr;  // LNW_PROF phase timestamps
+  size_t prof_cap = 0;                   // d_prof capacity in slots (grown to the launch grid)
   lnw_analytics ana{};                   // bound analytics buffers (lnw_set_analytics)
   unsigned long long *ctr = nullptr;     // bound work counters (lnw_set_counters)
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
@@ -3307,6 +3308,20 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   lnw_handle *h = new lnw_handle();
   h->device = device;
   if (const char *dbg = getenv("LNW_DEBUG_SKIP")) h->dbg_skip = atoi(dbg);
+#ifndef LNW_DIAG
+  // the shipped library honours only the knobs that change the launch shape or
+  // code path, never the results (bit 9: no quiet path, 17: per-lane bearing
+  // loop, 22/23: where the head's loads are issued); section skips and
+  // replaced arithmetic exist only in the diagnostics build (-DLNW_DIAG,
+  // lnw.build.build_diag)
+  constexpr int kResultPreserving = 512 | 131072 | 4194304 | 8388608;
+  if (h->dbg_skip & ~kResultPreserving) {
+    const int bad = h->dbg_skip & ~kResultPreserving;
+    delete h;
+    return fail(LNW_EINVAL, "LNW_DEBUG_SKIP bits " + std::to_string(bad) +
+                                " change results; they exist only in the diagnostics build (-DLNW_DIAG)");
+  }
+#endif
   h->prof = getenv("LNW_PROF") != nullptr;
   h->force_generic = getenv("LNW_FORCE_GENERIC") != nullptr;
   // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
@@ -3442,8 +3457,9 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   h->terrain = true;
   // dynamic LDS above the 64 KiB default needs an explicit opt-in
   {
-    size_t need = step_lds_bytes(h) + 1024;
-    if (need > 160 * 1024) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
+    const size_t need = step_lds_bytes(h);
+    // the same bound the launch attribute below grants
+    if (need > (size_t)GROUP_LDS_MAX) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     bool atan_lds;
     const size_t gneed = (size_t)group_lds_bytes(group_base(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16),
                                                    h->nb * h->nr, atan_lds) + 1024;
@@ -3451,11 +3467,13 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     // observed-list region: 1v1 is too small)
     h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX &&
                     h->nmax * (PAD * 4 + 2 * PADB) >= group_mask_bytes(h->nb * h->nr);
-    // the limit is per kernel function, shared by every handle of the process:
-    // set to the CU's whole LDS once, so a smaller handle never lowers it under
-    // a larger one's launch (the launch's own size sets the occupancy)
-    static bool lds_opt_in = false;
-    if (!lds_opt_in && (need > 64 * 1024 || gneed > 64 * 1024)) {
+    // the limit is per kernel function and device, shared by every handle of
+    // the process on that device: set to GROUP_LDS_MAX once per device, so a
+    // smaller handle never lowers it under a larger one's launch (the launch's
+    // own size sets the occupancy); hipSetDevice(h->device) above selects it
+    static unsigned long long lds_opt_in = 0;  // bit d: device d done
+    const unsigned long long dbit = 1ull << (h->device & 63);
+    if (!(lds_opt_in & dbit) && (need > 64 * 1024 || gneed > 64 * 1024)) {
       const void *ks[16] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
                             (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
                             (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
@@ -3466,7 +3484,7 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
                             (const void *)observe_kernel<3, 3, true>, (const void *)observe_kernel<4, 4, true>};
       for (const void *kk : ks)
         HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, GROUP_LDS_MAX));
-      lds_opt_in = true;
+      lds_opt_in |= dbit;
     }
   }
   (void)hipGetLastError();
@@ -3541,12 +3559,22 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
+  bool generic = h->force_generic;
+  const bool templated = k.los_mode != 2 && !generic && h->nb == h->nr && h->nb >= 2 && h->nb <= 4;
+  const bool use_group = k.los_mode != 2 && !templated && !generic && !h->no_group && h->group_fits;
+  // workgroups of the kernel launched below (the group kernel has its own grid)
+  const unsigned nwg = use_group ? (unsigned)((h->E + GEPW - 1) / GEPW) : grid.x;
   if (h->prof) {
-    if (!h->d_prof) HIPCHK(hipMalloc(&h->d_prof, (size_t)grid.x * PROF_SLOTS * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(h->d_prof, 0, (size_t)grid.x * PROF_SLOTS * sizeof(unsigned long long), st));
+    const size_t slots = (size_t)nwg * PROF_SLOTS;
+    if (slots > h->prof_cap) {
+      HIPCHK(hipStreamSynchronize(st));
+      if (h->d_prof) { (void)hipFree(h->d_prof); h->d_prof = nullptr; h->prof_cap = 0; }
+      HIPCHK(hipMalloc(&h->d_prof, slots * sizeof(unsigned long long)));
+      h->prof_cap = slots;
+    }
+    HIPCHK(hipMemsetAsync(h->d_prof, 0, slots * sizeof(unsigned long long), st));
     s.prof = h->d_prof;
   }
-  bool generic = h->force_generic;
 #define LNW_STEP(NB_, NR_, CW_, RW_)                                                             \
   step_kernel<NB_, NR_, CW_, RW_><<<grid, dim3(NB_ > 0 && EPW == WAVE ? 2 * WAVE : WAVE), lds, st>>>(k, s, actions_dev, row_kind_dev, obs_blue_dev, \
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
@@ -3556,7 +3584,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
   else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
   else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
-  else if (!generic && !h->no_group && h->group_fits) {
+  else if (use_group) {
     // runtime team sizes: GL lanes per env (lnw_group.inc)
     bool atan_lds;
     const size_t glds = (size_t)group_lds_bytes(
@@ -3569,7 +3597,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else LNW_STEP(0, 0, false, false);
 #undef LNW_STEP
   HIPCHK(hipGetLastError());
-  if (s.prof) prof_report(h, st, (int)grid.x);
+  if (s.prof) prof_report(h, st, (int)nwg);
   return 0;
 }
 

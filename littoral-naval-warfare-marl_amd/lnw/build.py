@@ -14,6 +14,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "liblnw.so")
+# diagnostics build: LNW_DEBUG_SKIP section skips (results change) and the
+# group kernel's section timers; never loaded unless LNW_LIB names it
+DIAG_OUT = os.path.join(HERE, "liblnw_diag.so")
+DIAG_DEFINES = ("LNW_DIAG", "LNW_GROUP_PROF")
 SOURCES = [os.path.join(CSRC, "lnw_kernels.hip"), os.path.join(CSRC, "lnw_actor.hip")]
 DEPS = SOURCES + [os.path.join(CSRC, "lnw_device.h"), os.path.join(CSRC, "lnw_quiet.inc"),
                   os.path.join(CSRC, "lnw_group.inc"),
@@ -63,5 +67,12 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     return out
 
 
+def build_diag(force=False, verbose=False):
+    return build(force=force, verbose=verbose, out=DIAG_OUT, defines=DIAG_DEFINES)
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--diag" in sys.argv:
+        print(build_diag(force="--force" in sys.argv, verbose=True))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

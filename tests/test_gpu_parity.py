@@ -776,3 +776,52 @@ def test_work_counters(grids):
     c = counts[2]
     assert c["rays_marched"] == 128 * 3 * E and c["astar_searches"] == 0, c
     assert 70 < c["cells_marched"] / c["rays_marched"] < 100, c
+
+
+def test_result_altering_debug_bits_refused(grids, monkeypatch):
+    """The shipped library refuses LNW_DEBUG_SKIP bits that change results
+    (section skips, replaced arithmetic): lnw_create fails loudly. The
+    timing-only bits (9: no quiet path, 17: per-lane bearings) are accepted."""
+    from lnw import _abi
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    for bits in ("1", str(1 << 16), str(1 << 21), str((1 << 9) | (1 << 20))):
+        monkeypatch.setenv("LNW_DEBUG_SKIP", bits)
+        with pytest.raises(_abi.LnwError, match="diagnostics build"):
+            BatchedGame(64, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+                        grid=grids[0], seed=1)
+    monkeypatch.setenv("LNW_DEBUG_SKIP", str((1 << 9) | (1 << 17)))
+    g = BatchedGame(64, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False),
+                    grid=grids[0], seed=1)
+    g.close()
+
+
+def test_prof_group_kernel_grid(grids, monkeypatch):
+    """LNW_PROF with the runtime-size group kernel, whose grid (E / 32
+    workgroups) is larger than the epw-64 step grid: the timestamp buffer is
+    sized by the launched grid (and regrown when a later launch needs more),
+    and the profiled launch gives the same results as an unprofiled one."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    sc = Scenario(landing_ops=True, auto_reset=True, episode_steps=40)
+    E = 2048
+    games = []
+    for prof in (True, False):
+        if prof:
+            monkeypatch.setenv("LNW_PROF", "1")
+        g = BatchedGame(E, ["small"] * 8, ["large"] * 8 + ["ls"] * 2, scenario=sc, grid=grids[1],
+                        seed=3)
+        monkeypatch.delenv("LNW_PROF", raising=False)
+        assert g.set_epw(64) == 64
+        g.reset(positions=[(0, 0)] * 18, rand_ls=[0] * 16 + [1, 1], box=((20, 60), (80, 140)))
+        games.append(g)
+    rng = np.random.default_rng(4)
+    for s in range(4):
+        act = torch.from_numpy(rng.random((E, 18, 4)).astype(np.float32)).cuda()
+        outs = [{k: v.cpu().numpy().copy() for k, v in g.step(act.clone()).items()} for g in games]
+        for k in outs[0]:
+            assert np.array_equal(outs[0][k], outs[1][k], equal_nan=True), (s, k)
+        if s == 1:
+            assert games[0].set_epw(8) == 8 and games[1].set_epw(8) == 8  # larger step grid
+    for g in games:
+        g.close()
