@@ -126,15 +126,18 @@ def make_game(E, env_base, spawns, los_mode, move_mode, cfg=None):
 
 
 def run_workload(E, env_base, spawns, los_mode, move_mode, steps, warmup, cfg=None, digest=False,
-                 count_steps=10):
+                 count_work=True):
     """Create the envs [env_base, env_base + E) of one rank, fill the actions of
     every step (Philox keyed by global env id and step, so a global env's
     inputs do not depend on the sharding), run `warmup` untimed steps, then
     time `steps` launches between barriers. Returns a dict: wall seconds, mean
     kernel ms from HIP events on the launch stream, envs with error bits,
-    episodes completed, the device work counters (rays / cells marched, A*
-    searches) per env-step over `count_steps` further, untimed steps, and with
-    `digest` the per-env final state."""
+    episodes completed, with `count_work` the device work counters (rays /
+    cells marched, A* searches, pooled bearings) per env-step over exactly the
+    timed window (a second, untimed pass that replays the same warmup and timed
+    steps from the same initial state with the counters bound: the step is
+    deterministic, so it walks the same trajectory), and with `digest` the
+    per-env final state."""
     from lnw import _abi
     L = _abi.load()
     g = make_game(E, env_base, spawns, los_mode, move_mode, cfg)
@@ -172,14 +175,25 @@ def run_workload(E, env_base, spawns, los_mode, move_mode, steps, warmup, cfg=No
     err = int((st["err"] != 0).sum())
     episodes = int(st["episode"].sum())
     work = None
-    if count_steps > 0 and not digest:
-        # untimed: the same kernels with the work counters bound (atomics)
+    if count_work and not digest:
+        # untimed replay of the same window with the work counters bound
+        # (atomics): a fresh game from the same seed and spawns, the warmup
+        # steps, then the timed steps counted
+        final = {k: st[k].copy() for k in ("rng", "episode", "steps_done")}
+        g.close()
+        g = make_game(E, env_base, spawns, los_mode, move_mode, cfg)
+        for s in range(warmup):
+            g.step(acts[s])
         g.count_work(True)
-        for s in range(count_steps):
-            g.step(acts[warmup + s % steps])
+        for s in range(steps):
+            g.step(acts[warmup + s])
         torch.cuda.synchronize()
-        work = {k: v / (E * count_steps) for k, v in g.work_counts().items()}
+        work = {k: v / (E * steps) for k, v in g.work_counts().items()}
         g.count_work(False)
+        st2 = g.env_state()
+        same = all(np.array_equal(final[k], st2[k]) for k in final)
+        work["window"] = (f"the {steps} timed steps (after {warmup} warmup steps), replayed "
+                          f"untimed with counters bound; same trajectory: {same}")
     dig = None
     if digest:
         ag = g.agents()
@@ -252,49 +266,59 @@ def ray_march(n=1 << 22, reps=10):
                 rays=n, mean_cells_per_ray=cells / n)
 
 
-def mappo_rollout(E=32768, T=40, reps=3):
-    """SURVEY.md §8(d) config 5 on one GPU: 40-step MAPPO rollouts of E envs, the
-    batched actor (network.py MLP) acting for every blue ship and the critic
-    scoring every step, interleaved with the step kernel (lnw.rollout.Rollout,
-    scripted red). env-steps/s including the policy forwards."""
+def mappo_rollout(total=32768, T=40, reps=3):
+    """40-step MAPPO rollouts of `total` envs over the
+    ranks (rank r holds lnw.shard.env_range's share, env_id_base = its first
+    global env), the batched actor (network.py MLP) acting for every blue ship
+    and the critic scoring every step, interleaved with the step kernel
+    (lnw.rollout.Rollout, scripted red). Each rank times its rollouts between
+    barriers; the slowest rank's time (max over ranks) sets the whole-job
+    env-steps/s, policy forwards included."""
+    from lnw import dist
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
     from lnw.rollout import BatchedActor, BatchedCritic, Rollout
+    world, rank, _ = dist.world()
+    lo, hi = dist.env_range(total, world, rank)
+    E = hi - lo
     sc = Scenario(landing_ops=False, tactics="aggressive", side="blue", trained_red=False,
                   auto_reset=True, episode_steps=40)
     g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc,
-                    device=torch.cuda.current_device(), seed=77)
+                    device=torch.cuda.current_device(), seed=77, env_id_base=lo)
     torch.manual_seed(0)
     actor = BatchedActor.for_obs(g.Db).cuda()
     critic = BatchedCritic(g.Db * g.nb).cuda()
-    gen = torch.Generator(device="cuda").manual_seed(5)
+    gen = torch.Generator(device="cuda").manual_seed(5 + rank)
     g.set_variant(True)  # scripted red closes in: contact most steps
     r = Rollout(g, actor, critic, steps=T, noise=0.05)
     g.reset(positions=REF_BLUE + REF_RED)
     r.run(generator=gen)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        g.reset(positions=REF_BLUE + REF_RED)
-        r.run(generator=gen)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
+
+    def timed(fn):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            g.reset(positions=REF_BLUE + REF_RED)
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        return dist.reduce_max([(time.perf_counter() - t0) / reps])[0]
+
+    dt = timed(lambda: r.run(generator=gen))
     # the same rollout replayed from a HIP graph (Rollout.capture): no host work
     # between the ~30 kernels of a step
     g.reset(positions=REF_BLUE + REF_RED)
     r.capture(generator=gen)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        g.reset(positions=REF_BLUE + REF_RED)
-        r.replay()
-    torch.cuda.synchronize()
-    dtg = (time.perf_counter() - t0) / reps
+    dtg = timed(r.replay)
     g.close()
-    return dict(env_steps_per_sec=E * T / dtg, ms_per_rollout=dtg * 1e3,
-                eager_env_steps_per_sec=E * T / dt, eager_ms_per_rollout=dt * 1e3, envs=E, steps=T,
+    return dict(env_steps_per_sec=total * T / dtg, ms_per_rollout=dtg * 1e3,
+                eager_env_steps_per_sec=total * T / dt, eager_ms_per_rollout=dt * 1e3,
+                envs=total, envs_per_gpu=E, n_gpus=world, steps=T,
                 policy="batched actor (network.py MLP) + critic (Value), fp32; HIP-graph replay "
-                       "(eager loop alongside)")
+                       "(eager loop alongside); max over ranks")
 
 
 def cpu_baseline(seconds, threads):
@@ -368,7 +392,10 @@ def secondary_lines(args):
             ("melee_65536", 65536, "melee", 0, 0,
              "65 536 4v4 envs, melee spawns (contact every step), contact kernel variant"),
             ("reference_march_astar", 65536, "reference", 1, 1,
-             "65 536 4v4 envs, reference spawns, every LOS query ray-marched, direct A*"),
+             "65 536 4v4 envs, reference spawns, direct A* for every move (no move table) and "
+             "LOS by ray march instead of the LOS table (los_mode 1); range pruning precedes "
+             "every LOS query, and at these spawns no pair is in sensor range, so no ray is "
+             "marched: this line measures direct A*"),
             ("reference_los_work", 65536, "reference", 2, 0,
              "65 536 4v4 envs, reference spawns, plus the reference's LOS work: every own x "
              "opponent Bresenham ray of every get_obs marched in full (los_mode 2)")):
@@ -419,6 +446,9 @@ def main():
     secondary = {}
     if world == 1 and not args.no_secondary and cfg is None:
         secondary = secondary_lines(args)
+    elif world > 1 and not args.no_secondary and cfg is None:
+        # config 5 is quoted on 8 GPUs: its 32 768 envs split over the ranks
+        secondary = {"config5_mappo_rollout": mappo_rollout()}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
@@ -451,6 +481,7 @@ def main():
                 "kernel_variant": "contact" if (cfg is None and args.spawns == "melee") else "default",
                 "los_mode": args.los_mode,
                 "move_mode": args.move_mode, "parallelism": f"env-shard x{world}",
+                "dist_backend": dist.backend(),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -473,8 +504,8 @@ def main():
                                 "marched_cells_per_env_step": w.get("cells_marched"),
                                 "marched_rays_per_env_step": w.get("rays_marched"),
                                 "astar_searches_per_env_step": w.get("astar_searches"),
-                                "counted_over": "10 untimed steps after the timed region, "
-                                                "rank 0, device counters (lnw_set_counters)"}
+                                "counted_over": "rank 0, device counters (lnw_set_counters): "
+                                                + str(w.get("window"))}
         if secondary:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)

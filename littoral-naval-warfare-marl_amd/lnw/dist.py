@@ -15,11 +15,17 @@ def world():
         int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def launched():
+    """True under a launcher (torch.distributed.run sets TORCHELASTIC_RUN_ID)."""
+    return "TORCHELASTIC_RUN_ID" in os.environ
+
+
 def init(backend=None):
-    """Initialise the default process group when launched with WORLD_SIZE > 1.
-    Returns (world_size, rank, local_rank)."""
+    """Initialise the default process group when launched with WORLD_SIZE > 1,
+    or under torch.distributed.run with one rank (the RCCL path then runs with
+    a world of one). Returns (world_size, rank, local_rank)."""
     ws, rank, local = world()
-    if ws > 1 and not dist.is_initialized():
+    if (ws > 1 or launched()) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         kw = {}
@@ -27,6 +33,11 @@ def init(backend=None):
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend, **kw)
     return ws, rank, local
+
+
+def backend():
+    """The process group's backend ("nccl" = RCCL on ROCm, "gloo"), or None."""
+    return dist.get_backend() if dist.is_initialized() else None
 
 
 def _dev():

@@ -113,21 +113,26 @@ class BatchedActor(nn.Module):
         x = torch.tanh(self.fc3(x))
         return torch.tanh(self.normal_head(x)), torch.exp(self.log_std_head(x))
 
-    def forward(self, obs, noise=None, bn="sample", generator=None):
+    def forward(self, obs, noise=None, bn="sample", generator=None, eps=None, noise_eps=None):
         """network.py:70-115 for every row: sample N(mean, std), add N(0, noise)
         exploration noise, clamp to [0, 1], log-probabilities of the clamped
         actions. Returns (actions, log_probs, ok) where ok marks rows without
-        NaN heads (the reference returns (None, None) for those)."""
+        NaN heads (the reference returns (None, None) for those). `eps` /
+        `noise_eps`: given standard-normal draws [B, n_outputs] instead of
+        drawing from `generator` (keyed_normal: shard-invariant rollouts)."""
         mean, std = self.heads(obs, bn)
         ok = ~(torch.isnan(mean).any(1) | torch.isnan(std).any(1))
         mean_s = torch.where(ok[:, None], mean, torch.zeros_like(mean))
         std_s = torch.where(ok[:, None], std, torch.ones_like(std))
         dist = Normal(mean_s, std_s, validate_args=False)  # no host sync (graph capture)
-        eps = torch.randn(mean.shape, generator=generator, device=mean.device, dtype=mean.dtype)
+        if eps is None:
+            eps = torch.randn(mean.shape, generator=generator, device=mean.device, dtype=mean.dtype)
         actions = mean_s + std_s * eps
         if noise is not None:
-            actions = actions + noise * torch.randn(mean.shape, generator=generator,
-                                                    device=mean.device, dtype=mean.dtype)
+            if noise_eps is None:
+                noise_eps = torch.randn(mean.shape, generator=generator, device=mean.device,
+                                        dtype=mean.dtype)
+            actions = actions + noise * noise_eps
         actions = torch.clamp(actions, 0, 1)
         return actions, dist.log_prob(actions), ok
 
@@ -161,6 +166,24 @@ class BatchedCritic(nn.Module):
         x = torch.tanh(self.fc2(x))
         x = torch.tanh(self.fc3(x))
         return self.fc4(x)
+
+
+def keyed_normal(row0, rows, cols, seed, slot, device):
+    """Standard-normal draws [rows, cols] for global rows row0 .. row0+rows-1,
+    a pure function of (seed, slot, global row, column): Philox uniforms
+    (lnw_fill_uniform_f32, the bench's action generator) at absolute counter
+    slot * 2^40 + row * 2 * cols + k, then Box-Muller. A rank holding global
+    envs [lo, hi) draws exactly the values one rank holding all envs draws for
+    them, so a sharded rollout samples what an unsharded one does."""
+    from . import _abi
+    L = _abi.load()
+    per = 2 * cols
+    u = torch.empty((rows, per), dtype=torch.float32, device=device)
+    off = (int(slot) << 40) + int(row0) * per
+    _abi.check(L.lnw_fill_uniform_f32(u.data_ptr(), rows * per, int(seed), off,
+                                      torch.cuda.current_stream(device).cuda_stream))
+    r = torch.sqrt(-2.0 * torch.log1p(-u[:, :cols]))  # 1 - u in (0, 1]
+    return r * torch.cos((2.0 * np.pi) * u[:, cols:])
 
 
 def red_script_table(device="cuda", dtype=torch.float64):
@@ -259,6 +282,12 @@ class Rollout:
       * sunk ships' action rows are stored as zeros (the reference stores the
         previous ship's `action` variable there, ppo.py:516-517).
 
+    `keyed_seed`: sampling draws come from keyed_normal (Philox keyed by the
+    global env id, the rollout index and the step) instead of a torch
+    generator, so a rollout sharded over ranks by env_id_base samples exactly
+    what one rank over all envs samples (eager runs; a captured graph freezes
+    the keys of the capture).
+
     `observe="step"` reuses the step's own output rows instead of a fresh
     observe (one launch less per step, but not the reference's draw order).
     `run(forced_actions=...)` replays given actor outputs [E, T, A, 4] instead of
@@ -268,9 +297,10 @@ class Rollout:
 
     def __init__(self, game: BatchedGame, actor, critic=None, steps=40, red="script",
                  red_actor=None, noise=None, bn="sample", red_bn="running", gamma=0.99,
-                 stop_at_done=True, observe="fresh"):
+                 stop_at_done=True, observe="fresh", keyed_seed=None):
         if observe not in ("fresh", "step"):
             raise ValueError("observe must be 'fresh' or 'step'")
+        self.keyed_seed, self._calls = keyed_seed, 0
         self.g, self.actor, self.critic = game, actor, critic
         self.T, self.red, self.red_actor = int(steps), red, red_actor
         self.noise, self.bn, self.red_bn = noise, bn, red_bn
@@ -278,7 +308,11 @@ class Rollout:
         self.table = red_script_table(game.device) if red == "script" else None
 
     @torch.no_grad()
-    def run(self, generator=None, forced_actions=None):
+    def run(self, generator=None, forced_actions=None, on_step=None):
+        """One rollout of T steps from the envs' current state. `on_step(t, out)`
+        is called after step t's launch with the step outputs (device tensors),
+        where ppo.py:620-638 does its per-step bookkeeping and logging; it must
+        not be given while capturing a graph if it synchronises."""
         from ._abi import F_ALIVE, LNW_KIND_F32, LNW_KIND_F64
         g = self.g
         E, nb, nr, A, D = g.E, g.nb, g.nr, g.A, g.Db
@@ -296,6 +330,17 @@ class Rollout:
         if self.observe == "step":
             g.observe(-1)
         live = torch.ones(E, dtype=torch.bool, device=dev)
+        call = self._calls
+        self._calls += 1
+        base = g.env_id_base
+
+        def draws(t, which, n_side):
+            """keyed draws for this step: which 0/1 blue sample / noise, 2 red"""
+            if self.keyed_seed is None:
+                return None
+            slot = ((call * T + t) * 4 + which)
+            return keyed_normal(base * n_side, E * n_side, 4, self.keyed_seed, slot, dev)
+
         for t in range(T):
             if self.observe == "fresh":
                 g.observe(-1)
@@ -309,7 +354,8 @@ class Rollout:
                                             bn=self.bn)
             else:
                 a, lp, _ = self.actor(cur.reshape(E * nb, D), noise=self.noise, bn=self.bn,
-                                      generator=generator)
+                                      generator=generator, eps=draws(t, 0, nb),
+                                      noise_eps=draws(t, 1, nb) if self.noise is not None else None)
             a = torch.where(ab, a.reshape(E, nb, 4), torch.zeros((), device=dev))
             acts[:, t] = a
             logp[:, t] = torch.where(ab, lp.reshape(E, nb, 4), torch.zeros((), device=dev))
@@ -323,7 +369,7 @@ class Rollout:
                     ra = forced_actions[:, t, nb:].to(torch.float32)
                 else:
                     ra, _, _ = self.red_actor(cur_red.reshape(E * nr, g.Dr), bn=self.red_bn,
-                                              generator=generator)
+                                              generator=generator, eps=draws(t, 2, nr))
                 full[:, nb:] = torch.where(ar, ra.reshape(E, nr, 4),
                                            torch.zeros((), device=dev)).double()
             else:
@@ -340,13 +386,13 @@ class Rollout:
             rew[:, t] = torch.where(live[:, None], r, torch.zeros_like(r)) if self.stop_at_done else r
             if self.stop_at_done:
                 live = live & (out["done"] != 0)
+            if on_step is not None:
+                on_step(t, out)
         rtg = reference_rtg(rew, self.gamma)
-        # a conventional GAE along each env's time axis over the mean ship
-        # reward; the reference learner instead applies gae() to (reward-to-go,
-        # value) pairs of a sampled minibatch (ppo.py:336), see `gae`
-        gae_time = gae(rew.mean(2), val.double(), self.gamma) if self.critic is not None else None
+        # the learner's advantage is gae(rtg, values) on a sampled minibatch
+        # (ppo.py:336), left to the caller as in the reference
         return dict(obs=obs, actions=acts, log_probs=logp, rewards=rew, values=val,
-                    running=running, f32_step=f32_step, rtg=rtg, gae_time=gae_time)
+                    running=running, f32_step=f32_step, rtg=rtg)
 
     def capture(self, generator=None):
         """Record one whole rollout (T steps of actor, red, critic, step kernel and

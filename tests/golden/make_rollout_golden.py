@@ -24,7 +24,7 @@ Recorded per scenario (R rollout episodes = R device envs):
                order instead of a sampled minibatch);
   weights      actor / critic / red actor state_dicts.
 
-usage: python tests/golden/make_rollout_golden.py    (writes rollout_*.npz)
+usage: python tests/golden/make_rollout_golden.py [NAME ...]   (writes rollout_*.npz)
 """
 import json
 import os
@@ -150,21 +150,36 @@ def run(name, *, n_blue, n_red, n_ls, landing_ops, trained_red, R, T, seed, boxe
           f"{[int(np.argmin(done[i])) if (done[i] == 0).any() else None for i in range(R)]}")
 
 
-def main():
+def main(only=None):
+    """All scenarios, or only the names given on the command line."""
     if not os.path.isdir(make_golden.REF):
         print("reference not present; nothing to do")
         return
+    if only is not None:
+        return _main_only(only)
+    _main_only(None)
+
+
+def _main_only(only):
     # untrained (scripted CSV) red, 3v3 at the reference spawns (game.py:551-585)
-    run("3v3_scripted", n_blue=3, n_red=3, n_ls=0, landing_ops=False, trained_red=False,
-        R=6, T=40, seed=31)
+    if only is None or "3v3_scripted" in only:
+        run("3v3_scripted", n_blue=3, n_red=3, n_ls=0, landing_ops=False, trained_red=False,
+            R=6, T=40, seed=31)
     # trained red (red actor in eval mode) with a landing ship and landing ops
-    run("4v2ls_trained", n_blue=4, n_red=2, n_ls=1, landing_ops=True, trained_red=True,
-        R=6, T=40, seed=32)
+    if only is None or "4v2ls_trained" in only:
+        run("4v2ls_trained", n_blue=4, n_red=2, n_ls=1, landing_ops=True, trained_red=True,
+            R=6, T=40, seed=32)
     # config 5's 4v4 through reset(..., blue_ships, red_ships), fleets 15-30 cells
     # apart, trained red: fire, sunk ships (float64 steps) and EW every episode
-    run("4v4_trained_contact", n_blue=4, n_red=4, n_ls=0, landing_ops=False, trained_red=True,
-        R=8, T=40, seed=33, boxes=(((30, 45), (40, 60)), ((55, 70), (45, 65))))
+    if only is None or "4v4_trained_contact" in only:
+        run("4v4_trained_contact", n_blue=4, n_red=4, n_ls=0, landing_ops=False, trained_red=True,
+            R=8, T=40, seed=33, boxes=(((30, 45), (40, 60)), ((55, 70), (45, 65))))
+    if only is None or "4v4_melee_done" in only:
+        # fleets 0-16 cells apart (the melee box): sinkings end most episodes
+        # before step 40 (done == 0, the `break` at ppo.py:640-641)
+        run("4v4_melee_done", n_blue=4, n_red=4, n_ls=0, landing_ops=False, trained_red=True,
+            R=8, T=40, seed=34, boxes=(((40, 48), (44, 56)), ((48, 56), (48, 60))))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

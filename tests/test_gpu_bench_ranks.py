@@ -67,4 +67,26 @@ def test_bench_main_two_ranks():
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["global_envs"] == 8192 and line["config"]["envs_per_gpu"] == 4096
     assert line["value"] == pytest.approx(8192 * 20 / (line["ms_per_step"] * 20 / 1e3), rel=1e-9)
-    assert line["err_envs"] == 0 and "secondary" not in line
+    assert line["err_envs"] == 0 and line["config"]["dist_backend"] == "gloo"
+    # at N > 1 the line carries config 5 split over the ranks
+    c5 = line["secondary"]["config5_mappo_rollout"]
+    assert list(line["secondary"]) == ["config5_mappo_rollout"]
+    assert c5["envs"] == 32768 and c5["envs_per_gpu"] == 16384 and c5["n_gpus"] == 2
+    assert c5["env_steps_per_sec"] == pytest.approx(32768 * 40 / (c5["ms_per_rollout"] / 1e3))
+
+
+def test_bench_main_rccl_one_rank():
+    """bench.py under torch.distributed.run with one rank: the process group
+    is RCCL ("nccl" backend) and the max-over-ranks all_reduce and barriers
+    the driver's N > 1 runs use go through it."""
+    env = dict(os.environ)
+    env.pop("LNW_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "20", "--warmup", "5", "--global-envs", "8192",
+           "--no-cpu-baseline", "--no-secondary"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert line["config"]["dist_backend"] == "nccl"
+    assert line["n_gpus"] == 1 and line["err_envs"] == 0 and line["value"] > 0

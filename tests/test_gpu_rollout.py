@@ -157,3 +157,50 @@ def test_rollout_graph_replay_matches_eager(E, T, contact):
     for k, v in eager.items():
         assert torch.equal(out[k], v), k
     g.close()
+
+
+def _port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rollout_ranks(tmp_path, world, total, red):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(root, "tests", "_rollout_rank.py"),
+                                       str(tmp_path / f"{red}_w{world}_r{r}.npz"), str(total), red],
+                                      env=env))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    return [np.load(tmp_path / f"{red}_w{world}_r{r}.npz") for r in range(world)]
+
+
+@pytest.mark.parametrize("red", ["script", "actor"])
+def test_rollout_shards_equal_one_rank(tmp_path, red):
+    """Config 5 sharded over ranks (bench.py's N > 1 line): two rank processes
+    (gloo, both on cuda:0), each a Rollout over its env_range half with
+    env_id_base = its first global env and keyed sampling, equal one rank over
+    all envs bit for bit: observations, actions, log-probabilities, rewards,
+    values, running masks and reward-to-go of two consecutive rollouts
+    (auto-reset, melee-box spawns: fire and sinkings)."""
+    total = 1024
+    one = _rollout_ranks(tmp_path, 1, total, red)[0]
+    two = _rollout_ranks(tmp_path, 2, total, red)
+    assert [(int(d["lo"]), int(d["hi"])) for d in two] == [(0, 512), (512, 1024)]
+    keys = [k for k in one.files if k not in ("lo", "hi")]
+    assert {"obs0", "actions1", "log_probs0", "rewards1", "values0", "rtg1", "running0"} <= set(keys)
+    for k in keys:
+        got = np.concatenate([d[k] for d in two])
+        assert np.array_equal(got, one[k], equal_nan=True), k
+    assert not one["running1"].all()  # some episodes ended inside a rollout

@@ -10,8 +10,11 @@ and step: the observations the actor saw (bit-exact float32), the action
 array's value kind after np.asarray (ppo.py:577), rewards (float64, 1e-5),
 log-probabilities and critic values (float32 network arithmetic on another
 device: 1e-4 / 1e-5), reward-to-go (ppo.py:645-659) and the learner's GAE
-(ppo.py:695-714 on the flattened batch) within 1e-5 relative, and the RNG
-tape consumed draw for draw."""
+(ppo.py:695-714 on the flattened batch, evaluated on the device) within 1e-5
+relative, and the RNG tape consumed draw for draw up to the step that ends the
+episode. `4v4_melee_done` has episodes that end before step 40 (done == 0 and
+the reference's `break`, ppo.py:640-641): the masking after it is checked
+against what the reference leaves in its buffers."""
 import json
 import os
 
@@ -26,7 +29,8 @@ pytestmark = pytest.mark.gpu
 NAMES = {0: "small", 1: "large", 2: "ls"}
 
 
-@pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact"])
+@pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact",
+                                  "4v4_melee_done"])
 def test_rollout_matches_reference(name):
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
@@ -61,11 +65,15 @@ def test_rollout_matches_reference(name):
         red_actor = BatchedActor.for_obs(g.Dr).load_reference(weights("red_actor.")).cuda()
     r = Rollout(g, actor, critic, steps=T, red="actor" if red_actor is not None else "script",
                 red_actor=red_actor, gamma=meta["gamma"])
-    out = r.run(forced_actions=torch.from_numpy(fx["act"]).cuda())
+    rng_after = []  # every env's draw counter after each step (the tape position)
+    out = r.run(forced_actions=torch.from_numpy(fx["act"]).cuda(),
+                on_step=lambda t, o: rng_after.append(g.env_state()["rng"].copy()))
     torch.cuda.synchronize()
     run = out["running"].cpu().numpy()
     n_steps = np.array(meta["n_steps"])
     assert np.array_equal(run.sum(1), n_steps)
+    if name == "4v4_melee_done":  # episodes that end early: the `break` at ppo.py:640-641
+        assert (n_steps < T).sum() >= 3, n_steps
     live = run[:, :, None, None]
     np.testing.assert_array_equal(np.where(live, out["obs"].cpu().numpy(), 0), fx["batch_obs"])
     np.testing.assert_array_equal(out["f32_step"].cpu().numpy() & run, fx["act_f32"].astype(bool))
@@ -77,13 +85,20 @@ def test_rollout_matches_reference(name):
                                fx["batch_values"], rtol=0, atol=1e-5)
     rtg = out["rtg"].cpu().numpy()
     np.testing.assert_allclose(rtg, fx["batch_rtg"][..., 0], rtol=1e-5, atol=1e-5)
-    # the learner's advantage (ppo.py:336) on the flattened batch, values from
-    # the device critic and reward-to-go from the device buffers
-    flat_v = torch.from_numpy(np.where(run, vals, 0)[:, :, None].repeat(nb, 2).reshape(1, -1))
-    adv = gae(out["rtg"].float().cpu().reshape(1, -1), flat_v, meta["gamma"])
-    np.testing.assert_allclose(adv.numpy().reshape(-1), fx["learner_gae"].reshape(-1), rtol=1e-5,
-                               atol=1e-5)
-    # every env consumed exactly its episode's draws
-    used = g.env_state()["rng"]
+    # the learner's advantage (ppo.py:336) on the flattened batch, computed on
+    # the device: values from the device critic (zero after the break, as the
+    # reference's buffer), reward-to-go from the device buffer (float32, as
+    # ppo.py:665 converts it)
+    run_d = out["running"]
+    flat_v = torch.where(run_d, out["values"], torch.zeros((), device=run_d.device))
+    flat_v = flat_v[:, :, None].expand(R, T, nb).reshape(1, -1)
+    assert flat_v.is_cuda and out["rtg"].is_cuda
+    adv = gae(out["rtg"].float().reshape(1, -1), flat_v, meta["gamma"])
+    assert adv.is_cuda
+    np.testing.assert_allclose(adv.cpu().numpy().reshape(-1), fx["learner_gae"].reshape(-1),
+                               rtol=1e-5, atol=1e-5)
+    # every env consumed exactly its episode's draws by the step that ended it
+    # (draws a finished env makes afterwards belong to no reference episode)
+    used = np.array([rng_after[n - 1][e] for e, n in enumerate(n_steps)])
     assert np.array_equal(used, [len(t) for t in tapes]), (used, [len(t) for t in tapes])
     g.close()
