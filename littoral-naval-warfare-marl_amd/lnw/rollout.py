@@ -270,8 +270,9 @@ class Rollout:
       4. the critic scores the concatenated blue observations (ppo.py:598-605).
 
     Rewards are kept in float64 (the reference's floats). With `stop_at_done`
-    an env's steps after its first done == 0 are masked out (rewards zeroed,
-    `running` False), as the reference `break`s and leaves zeros.
+    an env's steps after its first done == 0 are masked out (observations,
+    actions, log-probabilities, values and rewards zero, `running` False), as
+    the reference `break`s and leaves its buffers at zero.
 
     Differences from the reference loop, by design:
       * it observes the env it steps; ppo.py:497 calls get_obs on self.env, a
@@ -347,7 +348,11 @@ class Rollout:
             cur, cur_red = g.obs_blue, g.obs_red
             alive = g.get(F_ALIVE).t().bool()  # [E, A], slots not None
             ab = alive[:, :nb, None]
-            obs[:, t] = cur
+            # rows an env fills after its episode ended stay zero, as the
+            # reference's buffers do after its `break` (ppo.py:640-641)
+            keep = ab & live[:, None, None] if self.stop_at_done else ab
+            obs[:, t] = torch.where(live[:, None, None], cur, torch.zeros((), device=dev)) \
+                if self.stop_at_done else cur
             if forced_actions is not None:
                 a = forced_actions[:, t, :nb].to(torch.float32)
                 lp, _ = self.actor.get_dist(cur.reshape(E * nb, D), a.reshape(E * nb, 4),
@@ -357,8 +362,8 @@ class Rollout:
                                       generator=generator, eps=draws(t, 0, nb),
                                       noise_eps=draws(t, 1, nb) if self.noise is not None else None)
             a = torch.where(ab, a.reshape(E, nb, 4), torch.zeros((), device=dev))
-            acts[:, t] = a
-            logp[:, t] = torch.where(ab, lp.reshape(E, nb, 4), torch.zeros((), device=dev))
+            acts[:, t] = torch.where(keep, a, torch.zeros((), device=dev))
+            logp[:, t] = torch.where(keep, lp.reshape(E, nb, 4), torch.zeros((), device=dev))
             full[:, :nb] = a
             ar = alive[:, nb:, None]
             if self.red == "script":
@@ -379,7 +384,8 @@ class Rollout:
             f32_step[:, t] = f32
             kinds = torch.where(f32, LNW_KIND_F32, LNW_KIND_F64).to(torch.uint8)[:, None]
             if self.critic is not None:
-                val[:, t] = self.critic(cur.reshape(E, nb * D)).reshape(E)
+                v = self.critic(cur.reshape(E, nb * D)).reshape(E)
+                val[:, t] = torch.where(live, v, torch.zeros((), device=dev)) if self.stop_at_done else v
             out = g.step(full, kinds.expand(E, A).contiguous())
             running[:, t] = live
             r = out["rew_blue"].to(torch.float64)

@@ -53,10 +53,11 @@ def test_rollout_buffers():
     assert float(a.min()) >= 0 and float(a.max()) <= 1
     for k in ("obs", "log_probs", "values"):
         assert torch.isfinite(out[k]).all(), k
-    # the critic scored exactly the stored observations
+    # the critic scored exactly the stored observations (rows after an
+    # episode's end are zero in every buffer)
     with torch.no_grad():
         v = critic(out["obs"].reshape(E * T, -1)).reshape(E, T)
-    torch.testing.assert_close(v, out["values"])
+    torch.testing.assert_close(torch.where(out["running"], v, torch.zeros_like(v)), out["values"])
     # the final step's outputs are the live buffers of the game
     last = out["obs"][:, -1]
     assert torch.isfinite(last).all()

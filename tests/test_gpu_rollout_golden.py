@@ -74,24 +74,22 @@ def test_rollout_matches_reference(name):
     assert np.array_equal(run.sum(1), n_steps)
     if name == "4v4_melee_done":  # episodes that end early: the `break` at ppo.py:640-641
         assert (n_steps < T).sum() >= 3, n_steps
-    live = run[:, :, None, None]
-    np.testing.assert_array_equal(np.where(live, out["obs"].cpu().numpy(), 0), fx["batch_obs"])
+    # after an episode's `break` the device buffers hold zeros, like the reference's
+    np.testing.assert_array_equal(out["obs"].cpu().numpy(), fx["batch_obs"])
     np.testing.assert_array_equal(out["f32_step"].cpu().numpy() & run, fx["act_f32"].astype(bool))
     np.testing.assert_allclose(out["rewards"].cpu().numpy(), fx["rew"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(out["log_probs"].cpu().numpy(), fx["batch_log_probs"], rtol=0,
                                atol=1e-4)
     vals = out["values"].cpu().numpy()
-    np.testing.assert_allclose(np.where(run, vals, 0)[:, :, None, None].repeat(nb, 2),
-                               fx["batch_values"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(vals[:, :, None, None].repeat(nb, 2), fx["batch_values"], rtol=0,
+                               atol=1e-5)
     rtg = out["rtg"].cpu().numpy()
     np.testing.assert_allclose(rtg, fx["batch_rtg"][..., 0], rtol=1e-5, atol=1e-5)
     # the learner's advantage (ppo.py:336) on the flattened batch, computed on
     # the device: values from the device critic (zero after the break, as the
     # reference's buffer), reward-to-go from the device buffer (float32, as
     # ppo.py:665 converts it)
-    run_d = out["running"]
-    flat_v = torch.where(run_d, out["values"], torch.zeros((), device=run_d.device))
-    flat_v = flat_v[:, :, None].expand(R, T, nb).reshape(1, -1)
+    flat_v = out["values"][:, :, None].expand(R, T, nb).reshape(1, -1)
     assert flat_v.is_cuda and out["rtg"].is_cuda
     adv = gae(out["rtg"].float().reshape(1, -1), flat_v, meta["gamma"])
     assert adv.is_cuda
