@@ -58,6 +58,9 @@ struct LdsLayout {
   // pos_new, observed lists); qstage1 the scratch dead after phase W (rewards,
   // steps, missile kinds) plus the mask region; qlut sits at the very end.
   int qstage0, qstage1, qlut;
+  // small quiet workgroups (epw * nb <= 64, lnw_quiet.inc): one stage per side
+  // holding every row of the workgroup, appended after everything else
+  int qbig;
 };
 
 // Row staging for phase O: up to 64 observation rows. The row stride S (floats)
@@ -92,7 +95,7 @@ constexpr int QEPG = 8;
 __host__ __device__ constexpr int qstage_bytes(int ns) { return QEPG * ns * stage_stride(ns) * 4; }
 
 __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax, int mask_words,
-                                                int G) {
+                                                int G, int qbig_rows = 0) {
   LdsLayout L;
   int o = 0;
   L.pos_cur = o; o += A * PAD * 4;
@@ -140,6 +143,8 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   const int lut = ((G + 3) & ~3) * 4;
   if (o - L.qstage1 < qneed + lut) o = L.qstage1 + qneed + lut;
   L.qlut = o - lut;
+  L.qbig = o;
+  o += 2 * qbig_rows * stage_stride(nb) * 4;
   L.total = o;
   return L;
 }
@@ -150,7 +155,7 @@ struct Cols {
   double *reward, *act0, *act1;
   uint8_t *miss_cur, *miss_old, *mkind, *type, *alive0, *eng, *obsd, *bcnt, *border, *akind;
   uint32_t *mask;
-  float *stage, *estage, *qstage0, *qstage1, *qlut;
+  float *stage, *estage, *qstage0, *qstage1, *qlut, *qbig;
 };
 
 __device__ inline Cols carve(char *base, const LdsLayout &L) {
@@ -183,6 +188,7 @@ __device__ inline Cols carve(char *base, const LdsLayout &L) {
   c.qstage0 = (float *)(base + L.qstage0);
   c.qstage1 = (float *)(base + L.qstage1);
   c.qlut = (float *)(base + L.qlut);
+  c.qbig = (float *)(base + L.qbig);
   return c;
 }
 
@@ -2361,13 +2367,14 @@ __device__ inline void prof_stamp(const KState &S, int slot) {
 // landing-ops termination, episode counters, centre-of-gravity distance of the
 // pre-move positions, the per-env outputs, then phase W (state stored back, or
 // an in-kernel Game.reset when the episode ends).
-__device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols &c, int lane, int env,
-                                         int nb, int A, const Neut &N, int (&ev)[8],
-                                         const int (&hits)[2], int nbp, int nrp, int bsx, int bsy,
-                                         int rsx, int rsy, Rng &rng, float *rew_b, float *rew_r,
-                                         int32_t *done_out, float *cog_out) {
-  const long long E = P.E;
-  const int nr = A - nb;
+// The part of the tail every caller shares: team bonus, loss penalty, victory /
+// defeat and landing-ops checks on the reward columns, the env counters in ev,
+// the cog distance. Returns done (1 running, 0 terminal); *cog_p gets the cog
+// distance (NaN = None).
+__device__ __forceinline__ int env_tail_core(const KParams &P, Cols &c, int lane, int nb, int A,
+                                             const Neut &N, int (&ev)[8], const int (&hits)[2],
+                                             int nbp, int nrp, int bsx, int bsy, int rsx, int rsy,
+                                             double *cog_p) {
   int done = 1;
   double cog = NAN;
   // ---- tail (game.py:409-520) -------------------------------------------
@@ -2432,12 +2439,30 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
       }
     }
   }
-  int steps_env = ev[2] + 1;
-  ev[2] = steps_env;
+  ev[2] = ev[2] + 1;
   if (nbp > 0 && nrp > 0) {
     double bx = (double)bsx / nbp, by = (double)bsy / nbp, rx = (double)rsx / nrp, ry = (double)rsy / nrp;
     cog = sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
   }
+  *cog_p = cog;
+  return done;
+}
+
+// episode end: done == 0 or the horizon (the in-kernel auto-reset)
+__device__ __forceinline__ bool env_resets(const KParams &P, int done, int steps_env) {
+  return P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
+}
+
+__device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols &c, int lane, int env,
+                                         int nb, int A, const Neut &N, int (&ev)[8],
+                                         const int (&hits)[2], int nbp, int nrp, int bsx, int bsy,
+                                         int rsx, int rsy, Rng &rng, float *rew_b, float *rew_r,
+                                         int32_t *done_out, float *cog_out) {
+  const long long E = P.E;
+  const int nr = A - nb;
+  double cog;
+  const int done = env_tail_core(P, c, lane, nb, A, N, ev, hits, nbp, nrp, bsx, bsy, rsx, rsy, &cog);
+  const int steps_env = ev[2];
   // outputs
   // float32 values by default; float64 (the reference's Python floats) when
   // lnw_set_reward_dtype asked for it
@@ -2457,7 +2482,7 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
   if (done_out) done_out[env] = done;
   prof_stamp(S, 2);
   // ---- phase W: store state (alive updated by the neutralized lists) --
-  bool do_reset = P.auto_reset && (done == 0 || (P.episode_steps > 0 && steps_env >= P.episode_steps));
+  const bool do_reset = env_resets(P, done, steps_env);
   for (int a = 0; a < A; a++) {
     size_t ai = (size_t)a * E + env;
     int side = a >= nb;
@@ -2506,7 +2531,9 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   constexpr bool ST = NB > 0;
   const int nb = ST ? NB : P.nb, nr = ST ? NR : P.nr;
   const int A = nb + nr;
-  LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G);
+  // small quiet workgroups get whole-side row stages (quiet_step_t's direct mode)
+  const int qbig_rows = ST && NB == NR && EPW == WAVE && P.los_mode == 0 && epw * NB <= WAVE ? epw * NB : 0;
+  LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G, qbig_rows);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
   __shared__ int prog, qclaim;
@@ -2575,8 +2602,14 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
         __syncthreads();
       }
       if (wid == 0) prof_stamp(S, 7);
-      const bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
+      bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
       if (wid == 0) prof_stamp(S, 8);
+#ifdef LNW_DIAG
+      if (P.dbg_skip & (1 << 24)) {  // diagnostics: the quiet test again, its code now cached
+        wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane] + (P.dbg_skip >> 30)));
+        if (wid == 0) prof_stamp(S, 12);
+      }
+#endif
       if (wq) {
         quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
                              rew_r, done_out, cog_out, env0, nenv, valid);
@@ -3069,6 +3102,16 @@ size_t step_lds_bytes(const lnw_handle *h) {
   return (size_t)L.total;
 }
 
+// the step launch's LDS: step_lds_bytes plus the whole-side row stages of
+// small quiet workgroups (the same condition step_kernel evaluates)
+size_t step_launch_lds_bytes(const lnw_handle *h, int epw) {
+  const bool tmpl = !h->force_generic && h->params.los_mode == 0 && h->nb == h->nr && h->nb >= 2 &&
+                    h->nb <= 4 && EPW == WAVE;
+  const int rows = tmpl && epw * h->nb <= WAVE ? epw * h->nb : 0;
+  LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G, rows);
+  return (size_t)L.total;
+}
+
 // Environments per workgroup: EPW (one env per lane) unless that leaves the GPU
 // with fewer workgroups than it can hold at once; then halve it (down to 16 for
 // the two-wave kernels, 1 otherwise) until the grid fills every resident slot. A step is a per-lane latency chain, so a
@@ -3085,19 +3128,23 @@ int choose_epw(const lnw_handle *h) {
   if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
     ncu = prop.multiProcessorCount;
   const bool two_wave = !h->force_generic && h->params.los_mode != 2 && h->nb == h->nr && h->nb >= 2 && h->nb <= 4 && EPW == WAVE;
-  const size_t lds = step_lds_bytes(h) + 1024;
-  int per_cu = (int)((160 * 1024) / lds);
   const int by_waves = two_wave ? 4 : 8;  // 256 VGPRs: two waves per SIMD
-  if (per_cu > by_waves) per_cu = by_waves;
-  if (per_cu < 1) per_cu = 1;
-  const long long slots = (long long)ncu * per_cu;
+  // resident workgroups at a given epw (the launch's LDS depends on it: small
+  // quiet workgroups carry whole-side row stages)
+  auto slots = [&](int e) {
+    const size_t lds = step_launch_lds_bytes(h, e) + 1024;
+    int per_cu = (int)((160 * 1024) / lds);
+    if (per_cu > by_waves) per_cu = by_waves;
+    if (per_cu < 1) per_cu = 1;
+    return (long long)ncu * per_cu;
+  };
   // two-wave kernels stop at 16 envs per workgroup: below that each workgroup's
   // fixed head (terrain mask staging, state columns) outweighs the shorter
   // chain (8 192 envs: 20.2 us at 16, 20.5 at 8, 22.3 at 32, 29.0 at 64)
   const int min_epw = two_wave ? 16 : 1;
   int epw = EPW;
-  while (epw > min_epw && (h->E + epw - 1) / epw < slots) epw /= 2;
-  if ((h->E + epw - 1) / epw > slots && epw < EPW) epw *= 2;  // never more rounds than EPW needs
+  while (epw > min_epw && (h->E + epw - 1) / epw < slots(epw)) epw /= 2;
+  if ((h->E + epw - 1) / epw > slots(epw) && epw < EPW) epw *= 2;  // never more rounds than EPW needs
   return epw;
 }
 
@@ -3110,7 +3157,8 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
   if (hipMemcpyAsync(t.data(), h->d_prof, t.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return;
-  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0, sa[8] = {0}, sq[4] = {0}, sp[4] = {0}, sg[4] = {0};
+  double sL = 0, sM = 0, sS = 0, sW = 0, s1 = 0, sa[8] = {0}, sq[4] = {0}, sp[4] = {0}, sg[4] = {0},
+         st3[3] = {0, 0, 0};
   int nq = 0;
   unsigned long long t0 = ~0ull, tend0 = 0, tend1 = 0;
   int n1 = 0;
@@ -3129,6 +3177,11 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
       sq[1] += (double)(r[7] - r[6]);
       sq[2] += (double)(r[8] - r[7]);
       sq[3] += (double)(r[9] - r[8]);
+      if (r[10] && r[11]) {  // tail: rewards | cog | env_tail + outputs
+        st3[0] += (double)(r[10] - r[1]);
+        st3[1] += (double)(r[11] - r[10]);
+        st3[2] += (double)(r[2] - r[11]);
+      }
     } else {
       for (int a = 0; a < 8; a++)
         if (r[6 + a]) sa[a] += (double)(r[6 + a] - (a ? r[5 + a] : r[1]));
@@ -3259,9 +3312,20 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
     fprintf(stderr, "; block%%8==xcc for %d of %d\n",
             [&] { int k = 0; for (int w = 0; w < nwg; w++) k += (int)(t[(size_t)w * PROF_SLOTS + 30] & 15) == (w & 7); return k; }(), nwg);
   }
+  {
+    double rq = 0;
+    int nr2 = 0;
+    for (int w = 0; w < nwg; w++) {
+      const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+      if (r[14] && r[12] > r[8] && r[8]) { rq += (double)(r[12] - r[8]); nr2++; }
+    }
+    if (nr2) fprintf(stderr, "[lnw prof] repeated quiet test (diagnostics): %.2f us\n", rq / nr2 * us);
+  }
   if (nq)
-    fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us\n",
-            nq, sq[0] / nq * us, sq[1] / nq * us, sq[2] / nq * us, sq[3] / nq * us);
+    fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us; "
+                    "tail: rewards %.2f, cog %.2f, env_tail+outputs %.2f us\n",
+            nq, sq[0] / nq * us, sq[1] / nq * us, sq[2] / nq * us, sq[3] / nq * us, st3[0] / nq * us,
+            st3[1] / nq * us, st3[2] / nq * us);
   const int ns = nwg - nq;
   fprintf(stderr, "[lnw prof] phase S workgroups %d, per agent (us):", ns);
   for (int a = 0; a < 8; a++) fprintf(stderr, " %.2f", ns ? sa[a] / ns * us : 0.0);
@@ -3457,7 +3521,8 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   h->terrain = true;
   // dynamic LDS above the 64 KiB default needs an explicit opt-in
   {
-    const size_t need = step_lds_bytes(h);
+    // the largest step launch (64 / nb envs per workgroup: the biggest row stages)
+    const size_t need = step_launch_lds_bytes(h, WAVE / h->nb);
     // the same bound the launch attribute below grants
     if (need > (size_t)GROUP_LDS_MAX) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     bool atan_lds;
@@ -3556,7 +3621,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   k.act_dtype = action_dtype;
   k.dbg_skip = h->dbg_skip;
   KState s = make_state(h);
-  size_t lds = step_lds_bytes(h);
+  size_t lds = step_launch_lds_bytes(h, k.epw);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
   bool generic = h->force_generic;

@@ -584,10 +584,11 @@ def test_quiet_path_vs_oracle(grids, trained_red):
 @pytest.mark.parametrize("spawns", ["reference", "mixed"])
 def test_quiet_path_vs_phase_s_long(grids, spawns, trained_red, E, monkeypatch):
     """The bench workload shape (auto-reset, 40-step episodes, Philox) over 90
-    steps, three launch shapes with identical results (observations, rewards,
+    steps, four launch shapes with identical results (observations, rewards,
     done, cog, written-back actions, final state): 64 envs per workgroup (quiet
-    path where it applies), 8 envs per workgroup (the quiet path in partial
-    two-wave workgroups, the small-E launch shape), and 64 per workgroup with
+    path where it applies), 16 and 8 envs per workgroup (the quiet path in
+    partial two-wave workgroups with wave 1 storing every row straight from
+    registers: the small-E launch shapes), and 64 per workgroup with
     the quiet path disabled (LNW_DEBUG_SKIP bit 9: phase S everywhere). E = 8 192
     is config 3's per-GPU shard; 4 133 leaves a ragged last workgroup. "mixed":
     every second group of 64 envs spawns (and re-spawns) in the melee box."""
@@ -601,7 +602,7 @@ def test_quiet_path_vs_phase_s_long(grids, spawns, trained_red, E, monkeypatch):
             n = min(64, E - 64 * w)
             pos[64 * w:64 * w + n] = _melee_positions(grids[0], n, 4, 4, seed=w)
     games = []
-    for epw, skip in ((64, None), (8, None), (64, "512")):
+    for epw, skip in ((64, None), (16, None), (8, None), (64, "512")):
         if skip:
             monkeypatch.setenv("LNW_DEBUG_SKIP", skip)  # read once, by lnw_create
         g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grids[0], seed=9)
