@@ -38,6 +38,8 @@ namespace {
 #define LNW_EPW 64
 #endif
 constexpr int EPW = LNW_EPW;    // environments per wavefront (= per workgroup)
+constexpr int UNITS = 4;        // 64-env units per workgroup of the headline kernel (step_kernel UN)
+constexpr int UNITS_LDS_MAX = 156 * 1024;  // its dynamic LDS: the CU's 160 KiB less its static LDS
 constexpr int PAD = EPW + 1;    // padded LDS column stride (words) -> no bank conflicts
 constexpr int PADB = EPW + 4;   // byte-array stride
 
@@ -2091,12 +2093,13 @@ __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, c
 // The 2-bit terrain mask into LDS: 16-B loads, all of a thread's issued before
 // any is stored (a plain word loop waits out one L2 round trip per word).
 template <int NW>
-__device__ __forceinline__ void stage_mask(const KParams &P, const KState &S, uint32_t *dst) {
+__device__ __forceinline__ void stage_mask(const KParams &P, const KState &S, uint32_t *dst,
+                                           int tid = (int)threadIdx.x) {
   const int nw = P.G * P.W16, n4 = nw >> 2;
   const u32x4 *src4 = (const u32x4 *)S.mask2;
   u32x4 *dst4 = (u32x4 *)dst;
   constexpr int U = 4;
-  for (int i0 = threadIdx.x; i0 < n4; i0 += U * NW * WAVE) {
+  for (int i0 = tid; i0 < n4; i0 += U * NW * WAVE) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -2109,7 +2112,7 @@ __device__ __forceinline__ void stage_mask(const KParams &P, const KState &S, ui
       if (i < n4) dst4[i] = v[u];
     }
   }
-  for (int w = (n4 << 2) + (int)threadIdx.x; w < nw; w += NW * WAVE) dst[w] = S.mask2[w];
+  for (int w = (n4 << 2) + tid; w < nw; w += NW * WAVE) dst[w] = S.mask2[w];
 }
 
 // ---------------------------------------------------------------------------
@@ -2516,14 +2519,24 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // REFW: los_mode 2's reference LOS work (march_pairs_ref), a separate
 // instantiation of the runtime-size kernel so the production kernels carry none
 // of its code
-template <int NB, int NR, bool CW = false, bool REFW = false>
-__global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2 : 1) void step_kernel(
+// UN > 1 (templated team sizes, full 64-env units, LOS table mode): UN units of
+// 64 envs and two waves each share one workgroup (one per CU at UN = 4). Every
+// unit runs its own phases L, M, Q or S on its own LDS block; the quiet units'
+// observation passes go through one workgroup-wide queue that every free wave
+// of a quiet unit serves, so the CU's units finish their stream together
+// instead of 4-5 us apart (the spread of separate workgroups on one CU).
+template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1>
+__global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
+  static_assert(UN == 1 || (NB > 0 && EPW == WAVE && !REFW), "units need the two-wave templated kernel");
+  const int unit = UN > 1 ? (int)(threadIdx.x / (2 * WAVE)) : 0;
   const int lane = threadIdx.x & (WAVE - 1);
-  const int wid = threadIdx.x / WAVE;
+  const int wid = UN > 1 ? (int)((threadIdx.x / WAVE) & 1) : (int)(threadIdx.x / WAVE);
   const int epw = P.epw;
-  const int env0 = blockIdx.x * epw;
+  const int env0 = (blockIdx.x * UN + unit) * epw;
+  // LNW_PROF: one record per unit (prof_stamp writes S.prof[blockIdx.x * PROF_SLOTS + slot])
+  if (UN > 1 && S.prof) S.prof += (size_t)(blockIdx.x * (UN - 1) + unit) * PROF_SLOTS;
   const int env = env0 + lane;
   const long long E = P.E;
   const bool valid = lane < epw && env < E;
@@ -2534,10 +2547,16 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
   // small quiet workgroups get whole-side row stages (quiet_step_t's direct mode)
   const int qbig_rows = ST && NB == NR && EPW == WAVE && P.los_mode == 0 && epw * NB <= WAVE ? epw * NB : 0;
   LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G, qbig_rows);
-  Cols c = carve(lds_dyn, L);
-  __shared__ double duct_col[WAVE];
-  __shared__ int prog, qclaim;
-  __shared__ int r2col[WAVE];  // per-env max sensor reach^2 (max_range2)
+  const int lstride = (L.total + 15) & ~15;  // one LDS block per unit
+  Cols c = carve(lds_dyn + unit * lstride, L);
+  __shared__ double duct_all[UN][WAVE];
+  __shared__ int prog_all[UN], qclaim_all[UN];
+  __shared__ int r2_all[UN][WAVE];  // per-env max sensor reach^2 (max_range2)
+  __shared__ int ushare[2];         // UN > 1: [0] mask of quiet units, [1] shared pass counter
+  double *duct_col = duct_all[unit];
+  int &prog = prog_all[unit], &qclaim = qclaim_all[unit];
+  int *r2col = r2_all[unit];
+  if (UN > 1 && threadIdx.x == 0) { ushare[0] = 0; ushare[1] = 0; }  // (before phase L's barrier)
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
@@ -2562,7 +2581,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
     prof_put(S, 29, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4));
   }
 
-  stage_mask<NW>(P, S, c.mask);
+  stage_mask<NW>(P, S, c.mask, (int)threadIdx.x - unit * NW * WAVE);
   const uint32_t *mask = c.mask;
   load_state<NB + NR, NW>(P, S, c, lane, env, valid, wid);
   double duct = valid ? S.duct[env] : 1.0;
@@ -2611,10 +2630,16 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE : WAVE, NB > 0 ? 2
       }
 #endif
       if (wq) {
-        quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
-                             rew_r, done_out, cog_out, env0, nenv, valid);
+        if constexpr (UN > 1)
+          quiet_step_units_t<NB, NR, UN>(P, S, c, lds_dyn, L, lstride, unit, lane, env, wid, duct_all,
+                                         ushare, actions, obs_b, obs_r, rew_b, rew_r, done_out, cog_out,
+                                         env0, valid);
+        else
+          quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
+                               rew_r, done_out, cog_out, env0, nenv, valid);
         return;
       }
+      if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
     }
   }
   if (wid == 1) {
@@ -3052,7 +3077,8 @@ struct lnw_handle {
   unsigned long long *ctr = nullptr;     // bound work counters (lnw_set_counters)
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
-  bool prof = false, force_generic = false, no_group = false, group_fits = false;
+  bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
+  bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
@@ -3390,6 +3416,8 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->force_generic = getenv("LNW_FORCE_GENERIC") != nullptr;
   // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
+  // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
+  h->no_units = getenv("LNW_NO_UNITS") != nullptr;
   h->params = *params;
   h->E = n_envs; h->nb = nb; h->nr = nr; h->A = nb + nr;
   h->nmax = nb > nr ? nb : nr;
@@ -3538,7 +3566,9 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     // own size sets the occupancy); hipSetDevice(h->device) above selects it
     static unsigned long long lds_opt_in = 0;  // bit d: device d done
     const unsigned long long dbit = 1ull << (h->device & 63);
-    if (!(lds_opt_in & dbit) && (need > 64 * 1024 || gneed > 64 * 1024)) {
+    const size_t uneed = (size_t)UNITS * ((step_lds_bytes(h) + 15) & ~(size_t)15);
+    h->units_fit = uneed <= (size_t)UNITS_LDS_MAX;
+    if (!(lds_opt_in & dbit) && (need > 64 * 1024 || gneed > 64 * 1024 || uneed > 64 * 1024)) {
       const void *ks[16] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
                             (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
                             (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
@@ -3549,6 +3579,8 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
                             (const void *)observe_kernel<3, 3, true>, (const void *)observe_kernel<4, 4, true>};
       for (const void *kk : ks)
         HIPCHK(hipFuncSetAttribute(kk, hipFuncAttributeMaxDynamicSharedMemorySize, GROUP_LDS_MAX));
+      HIPCHK(hipFuncSetAttribute((const void *)step_kernel<4, 4, false, false, UNITS>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, UNITS_LDS_MAX));
       lds_opt_in |= dbit;
     }
   }
@@ -3627,7 +3659,11 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   bool generic = h->force_generic;
   const bool templated = k.los_mode != 2 && !generic && h->nb == h->nr && h->nb >= 2 && h->nb <= 4;
   const bool use_group = k.los_mode != 2 && !templated && !generic && !h->no_group && h->group_fits;
-  // workgroups of the kernel launched below (the group kernel has its own grid)
+  // 4v4 at 64 envs per workgroup in LOS-table mode, whole units (the headline):
+  // the units kernel (LNW_NO_UNITS keeps one unit per workgroup)
+  const bool units = templated && h->nb == 4 && !h->contact && !h->no_units && h->units_fit && k.epw == EPW &&
+                     k.los_mode == 0 && h->E % (EPW * UNITS) == 0 && !(h->dbg_skip & (1 | 2 | 512));
+  // per-unit records (LNW_PROF) of the kernel launched below (the group kernel has its own grid)
   const unsigned nwg = use_group ? (unsigned)((h->E + GEPW - 1) / GEPW) : grid.x;
   if (h->prof) {
     const size_t slots = (size_t)nwg * PROF_SLOTS;
@@ -3645,7 +3681,14 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
                                                  done_dev, cog_dev)
   const bool cw = h->contact;
-  if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
+  if (units) {
+    // 4 units of 64 envs per workgroup, one workgroup per CU (step_kernel UN)
+    step_kernel<4, 4, false, false, UNITS><<<dim3(h->E / (EPW * UNITS)), dim3(2 * WAVE * UNITS),
+                                             (size_t)UNITS * ((lds + 15) & ~(size_t)15), st>>>(
+        k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev,
+        cog_dev);
+  }
+  else if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
   else if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
   else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
   else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
