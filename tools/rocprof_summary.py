@@ -49,11 +49,36 @@ def counters(d, stem):
     return {k: sum(v) / len(v) for k, v in per.items()}
 
 
+def trace_only(tag, cmd, steps):
+    """profiles/<tag>_rocprof.md from a --kernel-trace --stats run alone: every
+    kernel's calls, mean and total time, and (given the number of env steps the
+    command ran) the time per step of each kernel family."""
+    d = os.path.join(OUT, tag)
+    stats = os.path.join(d, "kt", "kt_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    lines = [f"# rocprofv3 --kernel-trace --stats: {cmd}", "",
+             "| kernel | calls | avg us | total ms | % | us per env step |", "|---|---|---|---|---|---|"]
+    for r in rows:
+        t = float(r["TotalDurationNs"])
+        per = f"{t / 1e3 / steps:.1f}" if steps else "-"
+        lines.append(f"| {short(r['Name'])[:90]} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{t / 1e6:.2f} | {100 * t / tot:.1f} | {per} |")
+    if steps:
+        lines += ["", f"GPU kernel time per env step (all kernels): {tot / 1e3 / steps:.1f} us over {steps} steps"]
+    open(os.path.join(PROF, f"{tag}_rocprof.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
 def main():
     import hashlib
     import bench
     tag = sys.argv[1]
-    key = sys.argv[sys.argv.index("--key") + 1]
+    key = sys.argv[sys.argv.index("--key") + 1] if "--key" in sys.argv else None
+    if key is None:  # kernel trace only (config 5): the stats table and the per-step split
+        return trace_only(tag, sys.argv[sys.argv.index("--cmd") + 1] if "--cmd" in sys.argv else "",
+                          int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 0)
     cmd = sys.argv[sys.argv.index("--cmd") + 1] if "--cmd" in sys.argv else "bench.py"
     d = os.path.join(OUT, tag)
     stats = os.path.join(d, "kt", "kt_kernel_stats.csv")
