@@ -30,6 +30,22 @@ using namespace lnw;
 // native 4 x f32 vector: arrays of it stay in VGPRs (HIP's union-based float4
 // defeats SROA and lands such arrays in scratch)
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+// One 16-B observation store at float4 index i4 of a wave-uniform base.
+// Write-through (buffer_store sc1) when wt: the line leaves this XCC's L2
+// clean, so the launch does not end by writing back megabytes of dirty
+// observation lines at the kernel boundary (P.store_wt; the host enables it
+// only while every offset fits the 32-bit buffer range). Else a non-temporal
+// store.
+__device__ __forceinline__ void st_obs4(f32x4 *base, uint32_t i4, f32x4 v, bool wt) {
+  if (wt) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), rs, i4 * 16u, 0, 16 /* sc1 */);
+  } else {
+    __builtin_nontemporal_store(v, base + i4);
+  }
+}
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
@@ -1868,7 +1884,7 @@ __device__ inline void row_regs_t(const Cols &c, const double *duct_col, int el,
 
 template <int NS, int NPASS4, bool NT = true>
 __device__ inline void copy_side_t(const float *stage, float *out, float *dummy, int ne,
-                                   long long genv0) {
+                                   long long genv0, bool wt = false) {
   constexpr int D = 4 * NS + 52, D4 = D / 4, S4 = stage_stride(NS) / 4;
   constexpr int IT = (NPASS4 + WAVE - 1) / WAVE;
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1884,6 +1900,18 @@ __device__ inline void copy_side_t(const float *stage, float *out, float *dummy,
     v[u] = st4[r * S4 + c4];
   }
   __builtin_amdgcn_sched_barrier(0);
+  if (wt) {
+    // write-through stores (buffer_store sc1): the lines leave this XCC's L2
+    // clean, so the launch does not end by writing back megabytes of dirty
+    // observation lines; lanes past the block fall outside the buffer range
+    // and are dropped by the hardware
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, n4 * 16, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < IT; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v[u]), rs, (lane + u * WAVE) * 16, 0,
+                                             16 /* sc1 */);
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < IT; u++) {  // unconditional stores: masked-out lanes hit the sink
     const int i = lane + u * WAVE;
@@ -1935,8 +1963,8 @@ __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, C
     wave_lds_sync();
     if (g0 + EPG < nenv) prefetch(g0 + EPG);
     if (!(P.dbg_skip & 16)) {
-      copy_side_t<NB, EPG * NB * (4 * NB + 52) / 4>(stage_b, obs_b, S.dummy, ne, env0 + g0);
-      copy_side_t<NR, EPG * NR * (4 * NR + 52) / 4>(stage_r, obs_r, S.dummy, ne, env0 + g0);
+      copy_side_t<NB, EPG * NB * (4 * NB + 52) / 4>(stage_b, obs_b, S.dummy, ne, env0 + g0, P.store_wt);
+      copy_side_t<NR, EPG * NR * (4 * NR + 52) / 4>(stage_r, obs_r, S.dummy, ne, env0 + g0, P.store_wt);
     }
     wave_lds_sync();
   }
@@ -2048,10 +2076,10 @@ __device__ __forceinline__ void emit_rows_t(const KParams &P, const KState &S, c
       if (it >= n) break;
       const int i = it * WAVE + lane;
       const int r = i / n, cc = i - (i / n) * n;
-      f32x4 *dst = out4 + (size_t)r * NS * D4 + GB[g] + cc;
+      const uint32_t i4 = (uint32_t)(r * NS * D4 + GB[g] + cc);
       if (P.dbg_skip & 32) continue;
-      if (P.dbg_skip & 64) *dst = cv[it];
-      else __builtin_nontemporal_store(cv[it], dst);
+      if (P.dbg_skip & 64) out4[i4] = cv[it];
+      else st_obs4(out4, i4, cv[it], P.store_wt);
     }
   }
 }
@@ -3078,6 +3106,7 @@ struct lnw_handle {
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
   bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
+  bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
@@ -3418,6 +3447,13 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
+  // write-through observation stores (st_obs4) while a side's output fits the
+  // 32-bit buffer offsets; LNW_NO_STORE_WT keeps non-temporal stores (A/B)
+  {
+    const int ns = nb > nr ? nb : nr;
+    const double side_bytes = (double)n_envs * ns * (4 * ns + 52) * 4.0;
+    h->store_wt = getenv("LNW_NO_STORE_WT") == nullptr && side_bytes < 2147483648.0;
+  }
   h->params = *params;
   h->E = n_envs; h->nb = nb; h->nr = nr; h->A = nb + nr;
   h->nmax = nb > nr ? nb : nr;
@@ -3652,6 +3688,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   KParams k = h->kp;
   k.act_dtype = action_dtype;
   k.dbg_skip = h->dbg_skip;
+  k.store_wt = h->store_wt;
   KState s = make_state(h);
   size_t lds = step_launch_lds_bytes(h, k.epw);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
