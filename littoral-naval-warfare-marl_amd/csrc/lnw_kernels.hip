@@ -3591,11 +3591,9 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     if (need > (size_t)GROUP_LDS_MAX) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     bool atan_lds;
     const size_t gneed = (size_t)group_lds_bytes(group_base(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16),
-                                                   h->nb * h->nr, atan_lds) + 1024;
-    // (else runtime sizes stay on step_kernel<0, 0>; the pair masks need the
-    // observed-list region: 1v1 is too small)
-    h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX &&
-                    h->nmax * (PAD * 4 + 2 * PADB) >= group_mask_bytes(h->nb * h->nr);
+                                                   atan_lds) + 1024;
+    // (else runtime sizes stay on step_kernel<0, 0>)
+    h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX;
     // the limit is per kernel function and device, shared by every handle of
     // the process on that device: set to GROUP_LDS_MAX once per device, so a
     // smaller handle never lowers it under a larger one's launch (the launch's
@@ -3733,7 +3731,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
     // runtime team sizes: GL lanes per env (lnw_group.inc)
     bool atan_lds;
     const size_t glds = (size_t)group_lds_bytes(
-        group_base(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16), h->nb * h->nr, atan_lds);
+        group_base(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16), atan_lds);
     if (s.prof) fprintf(stderr, "[lnw prof] group kernel LDS %zu B, bearing table in LDS: %d\n", glds, (int)atan_lds);
     step_group_kernel<<<dim3((h->E + GEPW - 1) / GEPW), dim3(GEPW * GL), glds, st>>>(
         k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev,
