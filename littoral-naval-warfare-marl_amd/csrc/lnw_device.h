@@ -49,6 +49,7 @@ struct KParams {
   int box_lo[2], box_hi[2];
   int epw;            // environments per workgroup (<= EPW; fewer when E is small, to fill the CUs)
   int store_wt;       // observation stream stored write-through (sc1): no dirty lines left in L2 at the launch end
+  int atan_odd;       // the host's bearing table is odd in dy (degrees(atan2(-dy, dx)) == -degrees(atan2(dy, dx))): the group kernel stages its dy >= 0 half
   int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table
 };
 

@@ -1553,9 +1553,11 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
 }
 
 // calculate_reward (game.py:214-295) for agent a of the env in LDS column `lane`
+// dlz: the agent-major LDS copy of dist_lz the group kernel stages in phase L
+// (entry a * dlz_stride), else null (read from HBM)
 __device__ __forceinline__ double reward_core(const KParams &P, const KState &S, Cols &c, int lane,
                                               long long E, int env, int a, bool moved, bool engage,
-                                              int n_hit) {
+                                              int n_hit, const double *dlz = nullptr, int dlz_stride = 0) {
   size_t ai = (size_t)a * E + env;
   int steps = COLW(c.steps, a) + 1;
   COLW(c.steps, a) = steps;
@@ -1587,7 +1589,7 @@ __device__ __forceinline__ double reward_core(const KParams &P, const KState &S,
     int dx = x - P.lz_x, dy = y - P.lz_y;
     double dl = sqrt((double)(dx * dx + dy * dy));
     if (dl > 0) {
-      double cur = (P.dbg_skip & 2097152) ? 1e9 : S.dist_lz[ai];  // (bit 21: diagnostics)
+      double cur = (P.dbg_skip & 2097152) ? 1e9 : (dlz ? dlz[a * dlz_stride] : S.dist_lz[ai]);  // (bit 21: diagnostics)
       if (dl < cur) { r += 1.0; S.dist_lz[ai] = dl; }
       else r -= 1.0;
     } else {
@@ -3495,6 +3497,13 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
       for (int dx = -R_LOS; dx <= R_LOS; dx++)
         at[(size_t)(dy + R_LOS) * LOS_W + (dx + R_LOS)] = atan2((double)dy, (double)dx) * (180.0 / PY_PI);
     HIPCHK(hipMemcpy(h->d_atan, at.data(), at.size() * sizeof(double), hipMemcpyHostToDevice));
+    // odd in dy (glibc's atan2 is; checked, not assumed): the group kernel then
+    // keeps only the dy >= 0 rows in LDS and negates for dy < 0
+    bool odd = true;
+    for (int dy = 1; dy <= R_LOS; dy++)
+      for (int dx = -R_LOS; dx <= R_LOS; dx++)
+        odd = odd && at[(size_t)(R_LOS - dy) * LOS_W + (dx + R_LOS)] == -at[(size_t)(R_LOS + dy) * LOS_W + (dx + R_LOS)];
+    h->kp.atan_odd = odd ? 1 : 0;
   }
   KParams &k = h->kp;
   k.discrete = params->discrete; k.landing_ops = params->landing_ops;
@@ -3589,11 +3598,10 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     const size_t need = step_launch_lds_bytes(h, WAVE / h->nb);
     // the same bound the launch attribute below grants
     if (need > (size_t)GROUP_LDS_MAX) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
-    bool atan_lds;
-    const size_t gneed = (size_t)group_lds_bytes(group_base(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16),
-                                                   atan_lds) + 1024;
+    const LdsLayout GLy = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G);
+    const size_t gneed = (size_t)group_lds(GLy, h->G * h->W16, h->A, h->kp.atan_odd != 0).total + 1024;
     // (else runtime sizes stay on step_kernel<0, 0>)
-    h->group_fits = gneed - 1024 <= (size_t)GROUP_LDS_MAX;
+    h->group_fits = (size_t)group_base(GLy, h->G * h->W16) <= (size_t)GROUP_LDS_MAX;
     // the limit is per kernel function and device, shared by every handle of
     // the process on that device: set to GROUP_LDS_MAX once per device, so a
     // smaller handle never lowers it under a larger one's launch (the launch's
@@ -3729,10 +3737,12 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
   else if (use_group) {
     // runtime team sizes: GL lanes per env (lnw_group.inc)
-    bool atan_lds;
-    const size_t glds = (size_t)group_lds_bytes(
-        group_base(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16), atan_lds);
-    if (s.prof) fprintf(stderr, "[lnw prof] group kernel LDS %zu B, bearing table in LDS: %d\n", glds, (int)atan_lds);
+    const GroupLds gl = group_lds(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16,
+                                  h->A, k.atan_odd != 0);
+    const size_t glds = (size_t)gl.total;
+    if (s.prof)
+      fprintf(stderr, "[lnw prof] group kernel LDS %zu B (staged: target lists %d, dist_lz %d, bearing half table %d)\n",
+              glds, (int)(gl.tls >= 0), (int)(gl.dlz >= 0), (int)(gl.atab >= 0));
     step_group_kernel<<<dim3((h->E + GEPW - 1) / GEPW), dim3(GEPW * GL), glds, st>>>(
         k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev,
         done_dev, cog_dev);
