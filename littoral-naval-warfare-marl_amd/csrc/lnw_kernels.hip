@@ -3599,9 +3599,9 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     // the same bound the launch attribute below grants
     if (need > (size_t)GROUP_LDS_MAX) return fail(LNW_EUNSUPPORTED, "agent count needs more LDS than a CU has");
     const LdsLayout GLy = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G);
-    const size_t gneed = (size_t)group_lds(GLy, h->G * h->W16, h->A, h->kp.atan_odd != 0).total + 1024;
+    const size_t gneed = (size_t)group_lds(GLy, h->G * h->W16, h->A, h->nb * h->nr, h->kp.atan_odd != 0).total + 1024;
     // (else runtime sizes stay on step_kernel<0, 0>)
-    h->group_fits = (size_t)group_base(GLy, h->G * h->W16) <= (size_t)GROUP_LDS_MAX;
+    h->group_fits = group_lds(GLy, h->G * h->W16, h->A, h->nb * h->nr, h->kp.atan_odd != 0).ms >= 0;
     // the limit is per kernel function and device, shared by every handle of
     // the process on that device: set to GROUP_LDS_MAX once per device, so a
     // smaller handle never lowers it under a larger one's launch (the launch's
@@ -3738,11 +3738,11 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else if (use_group) {
     // runtime team sizes: GL lanes per env (lnw_group.inc)
     const GroupLds gl = group_lds(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16,
-                                  h->A, k.atan_odd != 0);
+                                  h->A, h->nb * h->nr, k.atan_odd != 0);
     const size_t glds = (size_t)gl.total;
     if (s.prof)
-      fprintf(stderr, "[lnw prof] group kernel LDS %zu B (staged: target lists %d, dist_lz %d, bearing half table %d)\n",
-              glds, (int)(gl.tls >= 0), (int)(gl.dlz >= 0), (int)(gl.atab >= 0));
+      fprintf(stderr, "[lnw prof] group kernel LDS %zu B (staged: target lists %d, dist_lz %d, bearing half table %d, pooled slopes %d)\n",
+              glds, (int)(gl.tls >= 0), (int)(gl.dlz >= 0), (int)(gl.atab >= 0), (int)(gl.ms >= 0));
     step_group_kernel<<<dim3((h->E + GEPW - 1) / GEPW), dim3(GEPW * GL), glds, st>>>(
         k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev,
         done_dev, cog_dev);
