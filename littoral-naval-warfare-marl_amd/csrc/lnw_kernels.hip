@@ -251,6 +251,9 @@ struct Ctx {
   // of the env's group in the group kernel (lnw_group.inc), whose other lanes
   // repeat the env's serial work in step
   bool leader = true;
+  // group kernel: this lane's index in its env's group and the group's first
+  // lane in the wave (fire_dev<true> tests the opponents across the group)
+  int gsub = 0, gsh = 0;
 #ifdef LNW_GROUP_PROF
   unsigned long long gp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // group-kernel section timers
 #endif
@@ -1464,11 +1467,23 @@ __device__ inline void los_prefetch_t(Ctx &X) {
 }
 
 // check_target (combatant.py:570-584): first live opponent within 3.5 cells
+template <bool GRP = false>
 __device__ inline int check_target_dev(Ctx &X, int side, int tx, int ty) {
   const KParams &P = X.P;
   Cols &c = X.c;
   const int lane = X.lane;
   int opp0 = side ? 0 : P.nb, opp1 = side ? P.nb : P.A;
+  if constexpr (GRP) {  // lane gsub of the env's group tests opponent opp0 + gsub; the first one found
+    const int j = opp0 + X.gsub;
+    bool hit = false;
+    if (j < opp1 && COLB(c.alive0, j)) {
+      const uint32_t pj = COLW(c.pos_cur, j);
+      const int dx = pos_x(pj) - tx, dy = pos_y(pj) - ty;
+      hit = dx * dx + dy * dy <= 12;
+    }
+    const uint32_t m = (uint32_t)(__ballot(hit) >> X.gsh) & 0xffffu;
+    return m ? opp0 + __builtin_ctz(m) : -1;
+  }
   for (int j = opp0; j < opp1; j++) {
     if (!COLB(c.alive0, j)) continue;
     uint32_t pj = COLW(c.pos_cur, j);
@@ -1484,12 +1499,13 @@ struct Neut {
 };
 
 // fire_missile (combatant.py:587-668) — returns hit
+template <bool GRP = false>
 __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int ksalvo, Neut &N) {
   const KParams &P = X.P;
   Cols &c = X.c;
   const int lane = X.lane;
   const int side = a >= P.nb;
-  int t = check_target_dev(X, side, tx, ty);
+  int t = check_target_dev<GRP>(X, side, tx, ty);
   if (t < 0) return false;
   uint32_t pt = COLW(c.pos_cur, t), pa = COLW(c.pos_cur, a);
   int dx = pos_x(pt) - pos_x(pa), dy = pos_y(pt) - pos_y(pa);
