@@ -679,7 +679,7 @@ __device__ __forceinline__ void march_pairs_ref(Ctx &X, int me) {
       if (!COLB(c.alive0, j)) continue;
       const uint32_t pj = COLW(c.pos_cur, j);
       int n = 0;
-      acc += los_march<false>(X.S.mask2, P.W16, pos_x(pi), pos_y(pi), pos_x(pj), pos_y(pj), &n);
+      acc += los_march<false>(X.mask, P.W16, pos_x(pi), pos_y(pi), pos_x(pj), pos_y(pj), &n);
       if (X.S.ctr) {
         atomicAdd(&X.S.ctr[0], 1ull);
         atomicAdd(&X.S.ctr[1], (unsigned long long)n);
@@ -2946,8 +2946,15 @@ __global__ __launch_bounds__(64) void build_move_table_kernel(const uint32_t *ma
 }
 
 // LOS table: for every origin cell and offset in [-40,40]^2, bit0 radar clear,
-// bit1 EW clear (full march, no early exit)
-__global__ void build_los_table_kernel(const uint32_t *mask2, int G, int W16, uint32_t *lostab) {
+// bit1 EW clear (full march, no early exit). The 2-bit terrain mask is staged
+// into LDS once per workgroup (mwords words, when it fits the launch's LDS),
+// so the 81 rays of every thread march from LDS.
+__global__ __launch_bounds__(256) void build_los_table_kernel(const uint32_t *mask2, int G, int W16,
+                                                              uint32_t *lostab, int mwords) {
+  uint32_t *lm = (uint32_t *)lds_dyn;
+  for (int w = threadIdx.x; w < mwords; w += blockDim.x) lm[w] = mask2[w];
+  __syncthreads();
+  const uint32_t *msk = mwords ? lm : mask2;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long n = (long long)G * G * LOS_W;
   if (i >= n) return;
@@ -2960,7 +2967,7 @@ __global__ void build_los_table_kernel(const uint32_t *mask2, int G, int W16, ui
     for (int c = 0; c < LOS_W; c++) {
       int y2 = y1 + c - R_LOS;
       if (y2 < 0 || y2 >= G) continue;
-      uint32_t b = los_march<false>(mask2, W16, x1, y1, x2, y2);
+      uint32_t b = los_march<false>(msk, W16, x1, y1, x2, y2);
       int col = c * 2;
       words[col >> 5] |= b << (col & 31);
     }
@@ -2973,8 +2980,80 @@ __global__ void build_los_table_kernel(const uint32_t *mask2, int G, int W16, ui
 // ---------------------------------------------------------------------------
 // unit kernels
 // ---------------------------------------------------------------------------
-__global__ void los_batch_kernel(const uint8_t *grid, int G, const int16_t *pairs, long long n,
-                                 int move_thr, int ew_thr, uint8_t *out) {
+// lnw_los_batch (combatant.py:436-456 per ray): every workgroup first builds the
+// grid's 2-bit terrain mask (bit0 cell > move_thr, bit1 cell > ew_thr) in LDS,
+// then its waves march their share of the rays from it. A lane whose ray has
+// ended takes the wave's next unclaimed ray (ballot + popcount of the lanes
+// asking), so a wave advances at its lanes' mean ray length instead of
+// waiting on its longest ray; a ray stops early once both bits are blocked
+// (the result cannot change).
+constexpr int LB_THREADS = 256, LB_RAYS_PER_WAVE = 1024;
+__global__ __launch_bounds__(LB_THREADS) void los_batch_kernel(const uint8_t *grid, int G, const int16_t *pairs,
+                                                               long long n, int move_thr, int ew_thr, uint8_t *out) {
+  const int W16 = (G + 15) >> 4;
+  uint32_t *lm = (uint32_t *)lds_dyn;
+  for (int w = threadIdx.x; w < G * W16; w += LB_THREADS) {
+    const int x = w / W16, y0 = (w - x * W16) * 16;
+    uint32_t v = 0;
+    for (int b = 0; b < 16 && y0 + b < G; b++) {
+      const uint8_t g = grid[(size_t)x * G + y0 + b];
+      v |= ((g > move_thr ? 1u : 0u) | (g > ew_thr ? 2u : 0u)) << (2 * b);
+    }
+    lm[w] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (WAVE - 1);
+  const long long w0 = ((long long)blockIdx.x * (LB_THREADS / WAVE) + (threadIdx.x / WAVE)) * LB_RAYS_PER_WAVE;
+  const long long wend = w0 + LB_RAYS_PER_WAVE < n ? w0 + LB_RAYS_PER_WAVE : n;
+  long long next = w0;  // the wave's next unclaimed ray (uniform)
+  long long idx = -1;   // this lane's ray
+  int x = 0, y = 0, x2 = 0, y2 = 0, dx = 0, dy = 0, sx = 1, sy = 1, err = 0;
+  uint32_t blk = 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  auto claim = [&]() {
+    const unsigned long long need = __ballot(idx < 0);
+    if (idx < 0) {
+      const long long k = next + __popcll(need & below);
+      if (k < wend) {
+        const uint64_t pr = *(const uint64_t *)(pairs + 4 * k);
+        x = (int16_t)(pr & 0xffffu);
+        y = (int16_t)((pr >> 16) & 0xffffu);
+        x2 = (int16_t)((pr >> 32) & 0xffffu);
+        y2 = (int16_t)(pr >> 48);
+        dx = abs(x2 - x);
+        dy = abs(y2 - y);
+        sx = x > x2 ? -1 : 1;
+        sy = y > y2 ? -1 : 1;
+        err = dx - dy;
+        blk = 0;
+        idx = k;
+      }
+    }
+    next += __popcll(need);
+  };
+  claim();
+  while (__any(idx >= 0)) {
+    if (idx >= 0) {
+#pragma unroll 4
+      for (int s = 0; s < 8; s++) {
+        blk |= cell_bits(lm, W16, x, y);
+        if (blk == 3u || (x == x2 && y == y2)) {
+          out[idx] = (uint8_t)((~blk) & 3u);
+          idx = -1;
+          break;
+        }
+        const int e2 = 2 * err;
+        if (e2 > -dy) { err -= dy; x += sx; }
+        if (e2 < dx) { err += dx; y += sy; }
+      }
+    }
+    if (next < wend) claim();
+  }
+}
+
+// grids whose mask does not fit the launch's LDS: one lane per ray from HBM
+__global__ void los_batch_global_kernel(const uint8_t *grid, int G, const int16_t *pairs, long long n,
+                                        int move_thr, int ew_thr, uint8_t *out) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int x1 = pairs[4 * i], y1 = pairs[4 * i + 1], x2 = pairs[4 * i + 2], y2 = pairs[4 * i + 3];
@@ -3604,7 +3683,9 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   build_move_table_kernel<<<(unsigned)((nm + WAVE - 1) / WAVE), WAVE>>>(h->d_mask2, G, h->W16, h->d_mvtab);
   HIPCHK(hipGetLastError());
   long long nl = (long long)G * G * LOS_W;
-  build_los_table_kernel<<<(unsigned)((nl + 255) / 256), 256>>>(h->d_mask2, G, h->W16, h->d_lostab);
+  const int mwords = G * h->W16 * 4 <= 64 * 1024 ? G * h->W16 : 0;  // terrain mask staged in LDS
+  build_los_table_kernel<<<(unsigned)((nl + 255) / 256), 256, (size_t)mwords * 4>>>(h->d_mask2, G, h->W16,
+                                                                                     h->d_lostab, mwords);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   h->terrain = true;
@@ -3846,8 +3927,15 @@ int lnw_los_batch(const uint8_t *grid_dev, int32_t G, const int16_t *pairs_dev, 
                   int32_t move_thr, int32_t ew_thr, uint8_t *out_dev, void *stream) {
   if (!grid_dev || !pairs_dev || !out_dev) return fail(LNW_EINVAL, "null argument");
   if (n <= 0) return 0;
-  los_batch_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      grid_dev, G, pairs_dev, n, move_thr, ew_thr, out_dev);
+  const size_t lds = (size_t)G * ((G + 15) / 16) * 4;
+  if (lds <= 64 * 1024) {
+    const long long per_block = (long long)(LB_THREADS / WAVE) * LB_RAYS_PER_WAVE;
+    los_batch_kernel<<<(unsigned)((n + per_block - 1) / per_block), LB_THREADS, lds, (hipStream_t)stream>>>(
+        grid_dev, G, pairs_dev, n, move_thr, ew_thr, out_dev);
+  } else {
+    los_batch_global_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        grid_dev, G, pairs_dev, n, move_thr, ew_thr, out_dev);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }
