@@ -246,6 +246,10 @@ struct Ctx {
   // v = own ship i at its new cell. Valid when `pre` is set.
   uint64_t lpre[2];
   bool pre;
+  // contact variant (pair_tables_t): per side, pair b = i * NOPP + j (own-major)
+  // at bit b (own ship i on its start cell) and 16 + b (on its new cell):
+  // radar-detect possible / close / EW candidate, LOS included
+  uint32_t ptr_[2] = {0u, 0u}, ptc[2] = {0u, 0u}, ptw[2] = {0u, 0u};
   // the lane that makes the env's shared-counter side effects (analytics
   // records and maps): every lane where one lane steps one env; the first lane
   // of the env's group in the group kernel (lnw_group.inc), whose other lanes
@@ -1294,49 +1298,25 @@ __device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp
   Cols &c = X.c;
   const int lane = X.lane;
   const int myradar = COLW(c.radar_cur, me);
-  uint32_t po[NOWN], pp[NOPP];
-  uint32_t tbits = 0;  // 2 bits per ship type: own ships at bit 2i, opponents at 2(NOWN+j)
-  uint32_t amask = 0, orad = 0, onew = 0;
+  uint32_t pp[NOPP];
+  uint32_t amask = 0, rowsel = 0;
 #pragma unroll
   for (int i = 0; i < NOWN; i++) {
-    po[i] = COLW(c.pos_cur, own0 + i);
-    tbits |= (uint32_t)COLB(c.type, own0 + i) << (2 * i);
-    amask |= (COLB(c.alive0, own0 + i) ? 1u : 0u) << i;
     // own ship i stands on its new cell once its turn has come and it moved
-    onew |= ((own0 + i <= me) && (COLW(c.pos_new, own0 + i) & 0x80000000u) ? 1u : 0u) << i;
+    const bool nw = (own0 + i <= me) && (COLW(c.pos_new, own0 + i) & 0x80000000u);
+    rowsel |= nw ? ((1u << NOPP) - 1u) << (i * NOPP) : 0u;
   }
 #pragma unroll
   for (int j = 0; j < NOPP; j++) {
     pp[j] = COLW(c.pos_cur, opp0 + j);
-    tbits |= (uint32_t)COLB(c.type, opp0 + j) << (2 * (NOWN + j));
     amask |= (COLB(c.alive0, opp0 + j) ? 1u : 0u) << (NOWN + j);
-    orad |= (COLW(c.radar_cur, opp0 + j) == 1 ? 1u : 0u) << j;
   }
   const unsigned long long tw = prof_now(X.S);
-  const double duct = X.duct();
-  const uint64_t lbits = X.lpre[own0 != 0];
-  uint32_t detm = 0, ewm = 0;
-#pragma unroll
-  for (int i = 0; i < NOWN; i++)
-#pragma unroll
-    for (int j = 0; j < NOPP; j++) {
-      const int b = i * NOPP + j;
-      const int dx = pos_x(pp[j]) - pos_x(po[i]), dy = pos_y(pp[j]) - pos_y(po[i]);
-      const int d2 = dx * dx + dy * dy;
-      const bool in = ((amask >> i) & (amask >> (NOWN + j)) & 1u) && d2 < X.r2max;
-      const int ti = (tbits >> (2 * i)) & 3u, tj = (tbits >> (2 * (NOWN + j))) & 3u;
-      const int rr = radar_r(X.P, duct, ti, tj), re = ew_r(X.P, duct, ti, tj);
-      const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
-      const bool ew_cand = d2 < re * re && ((orad >> j) & 1u);
-      uint32_t los = 0;
-      if (X.pre) {
-        los = (uint32_t)(lbits >> ((b * 2 + ((onew >> i) & 1u)) * 2)) & 3u;
-      } else if (in && (rad_ok || close || ew_cand)) {  // LOS result would be unused otherwise
-        los = los_q(X.P, X.S, X.mask, pos_x(po[i]), pos_y(po[i]), pos_x(pp[j]), pos_y(pp[j]));
-      }
-      detm |= (in && (rad_ok || close) && (los & 1u)) ? 1u << b : 0u;
-      ewm |= (in && ew_cand && (los & 3u) == 3u) ? 1u << b : 0u;
-    }
+  // the pair tables of this side (pair_tables_t), each pair on the cell its own ship stands on now
+  const int sd = own0 != 0;
+  auto sel = [&](uint32_t b) { return (b & 0xffffu & ~rowsel) | ((b >> 16) & rowsel); };
+  const uint32_t detm = sel(sd ? X.ptc[1] : X.ptc[0]) | (myradar == 1 ? sel(sd ? X.ptr_[1] : X.ptr_[0]) : 0u);
+  const uint32_t ewm = sel(sd ? X.ptw[1] : X.ptw[0]);
   uint32_t colj = 0;  // bits of opponent 0's column
 #pragma unroll
   for (int i = 0; i < NOWN; i++) colj |= 1u << (i * NOPP);
@@ -1463,6 +1443,147 @@ __device__ inline void los_prefetch_t(Ctx &X) {
   }
   X.lpre[0] = bits[0];
   X.lpre[1] = bits[1];
+  X.pre = true;
+}
+
+// Contact variant: every pair condition get_obs can ask for during this step's
+// agent loop, evaluated once before it (the pair tables, Ctx::ptr_/ptc/ptw).
+// Besides the cells (as los_prefetch_t: blue old/new x red old while blue
+// plays, red old/new x blue final while red plays), the rest is fixed for the
+// step too: types, ducting, alive flags (hits sink ships only in the tail) and
+// the opponents' radar states (red's before the step; blue's as take_action
+// sets it, rint(a0) or 0). Only the observer's own radar (radar-detect needs
+// it on) and the turn order (which own cell) are applied in get_obs_mask_t.
+// STEP = false (observe kernel): no ship moves and every radar is current.
+template <int NB, int NR, bool STEP>
+__device__ inline void pair_tables_t(Ctx &X) {
+  const KParams &P = X.P;
+  const KState &S = X.S;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  constexpr int NPAIR = NB * NR;
+  static_assert(NPAIR <= 16, "pair tables are 16 bits per cell version");
+  const double duct = X.duct();
+  int bo[NB], bn[NB], ro[NR], rn[NR];  // packed x<<8|y cells: old, final
+  uint32_t bmv = 0, rmv = 0, al = 0, tb = 0, tr = 0, radr = 0, radb = 0;
+#pragma unroll
+  for (int i = 0; i < NB; i++) {
+    const uint32_t po = COLW(c.pos_cur, i), pn = COLW(c.pos_new, i);
+    const bool mv = STEP && (pn & 0x80000000u) != 0;
+    bo[i] = pos_x(po) << 8 | pos_y(po);
+    bn[i] = mv ? (pos_x(pn & 0x7fffffffu) << 8 | pos_y(pn & 0x7fffffffu)) : bo[i];
+    bmv |= (mv ? 1u : 0u) << i;
+    al |= (COLB(c.alive0, i) ? 1u : 0u) << i;
+    tb |= (uint32_t)COLB(c.type, i) << (2 * i);
+    int rb;
+    if constexpr (STEP) {  // blue's radar once it has acted (take_action)
+      const double a0 = COLW(c.act0, i);
+      rb = isfinite(a0) ? (int)fmin(fmax(rint(a0), -2147483648.0), 2147483647.0) : 0;
+    } else {
+      rb = COLW(c.radar_cur, i);
+    }
+    radb |= (rb == 1 ? 1u : 0u) << i;
+  }
+#pragma unroll
+  for (int j = 0; j < NR; j++) {
+    const uint32_t po = COLW(c.pos_cur, NB + j), pn = COLW(c.pos_new, NB + j);
+    const bool mv = STEP && (pn & 0x80000000u) != 0;
+    ro[j] = pos_x(po) << 8 | pos_y(po);
+    rn[j] = mv ? (pos_x(pn & 0x7fffffffu) << 8 | pos_y(pn & 0x7fffffffu)) : ro[j];
+    rmv |= (mv ? 1u : 0u) << j;
+    al |= (COLB(c.alive0, NB + j) ? 1u : 0u) << (NB + j);
+    tr |= (uint32_t)COLB(c.type, NB + j) << (2 * j);
+    radr |= (COLW(c.radar_cur, NB + j) == 1 ? 1u : 0u) << j;  // red's radar before the step
+  }
+  // ray r: side s = r / (2*NPAIR); within a side q = (own*NOPP + opp)*2 + v
+  auto ray = [&](int r, int &x1, int &y1, int &x2, int &y2, uint32_t &f) {
+    const int s = r / (2 * NPAIR), q = r % (2 * NPAIR), v = q & 1, p = q >> 1;
+    int o, d, ti, tj;
+    bool need, radj;
+    if (s == 0) {
+      const int i = p / NR, j = p % NR;
+      o = v ? bn[i] : bo[i];
+      d = ro[j];
+      need = ((al >> i) & (al >> (NB + j)) & 1u) && (v == 0 || ((bmv >> i) & 1u));
+      ti = (tb >> (2 * i)) & 3u;
+      tj = (tr >> (2 * j)) & 3u;
+      radj = (radr >> j) & 1u;
+    } else {
+      const int j = p / NB, i = p % NB;
+      o = v ? rn[j] : ro[j];
+      d = bn[i];
+      need = ((al >> i) & (al >> (NB + j)) & 1u) && (v == 0 || ((rmv >> j) & 1u));
+      ti = (tr >> (2 * j)) & 3u;
+      tj = (tb >> (2 * i)) & 3u;
+      radj = (radb >> i) & 1u;
+    }
+    x1 = o >> 8; y1 = o & 255; x2 = d >> 8; y2 = d & 255;
+    const int dx = x2 - x1, dy = y2 - y1, d2 = dx * dx + dy * dy;
+    f = 0;
+    if (need && d2 < X.r2max) {
+      const int rr = radar_r(P, duct, ti, tj), re = ew_r(P, duct, ti, tj);
+      f = (d2 < rr * rr ? 1u : 0u) | (d2 < 16 ? 2u : 0u) | (d2 < re * re && radj ? 4u : 0u);
+    }
+  };
+  uint32_t tR[2] = {0u, 0u}, tC[2] = {0u, 0u}, tW[2] = {0u, 0u};
+  constexpr int NRAY = 4 * NPAIR;
+  constexpr int CH = 16;
+#pragma unroll
+  for (int r0 = 0; r0 < NRAY; r0 += CH) {
+    uint32_t wi[CH], tabm = 0, marchm = 0;
+    uint64_t fl = 0;  // 3 range bits per ray of the chunk
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      wi[u] = 0;
+      if (r0 + u >= NRAY) continue;
+      int x1, y1, x2, y2;
+      uint32_t f;
+      ray(r0 + u, x1, y1, x2, y2, f);
+      fl |= (uint64_t)f << (3 * u);
+      const int dx = x2 - x1, dy = y2 - y1;
+      const bool tab = P.los_mode != 1 && dx >= -R_LOS && dx <= R_LOS && dy >= -R_LOS && dy <= R_LOS;
+      tabm |= (f && tab ? 1u : 0u) << u;
+      marchm |= (f && !tab ? 1u : 0u) << u;
+      wi[u] = ((uint32_t)(x1 * P.G + y1) * LOS_CELL_WORDS + (dx + R_LOS) * LOS_ROW_WORDS) * 32u +
+              (dy + R_LOS) * 2;
+    }
+    uint64_t lb = 0;  // 2 LOS bits per ray of the chunk
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      if (r0 + u >= NRAY) continue;
+      const uint32_t w = (tabm >> u) & 1u ? S.lostab[wi[u] >> 5] : 0u;
+      lb |= (uint64_t)((w >> (wi[u] & 31)) & 3u) << (2 * u);
+    }
+    while (marchm) {  // outside the table window (very long sensor ranges), or march mode
+      const int u = __builtin_ctz(marchm);
+      marchm &= marchm - 1;
+      // the ray's cells again from the LDS columns: a runtime index into the
+      // register arrays above would put them in scratch for the whole function
+      const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR), v = q & 1, p = q >> 1;
+      const int o = s == 0 ? p / NR : NB + p / NB, d = s == 0 ? NB + p % NR : p % NB;
+      const uint32_t pn = COLW(c.pos_new, o);
+      const uint32_t po = STEP && v && (pn & 0x80000000u) ? (pn & 0x7fffffffu) : COLW(c.pos_cur, o);
+      uint32_t pd = COLW(c.pos_cur, d);
+      if (STEP && s == 1) {  // red -> blue rays end at the blue ship's final cell
+        const uint32_t qn = COLW(c.pos_new, d);
+        if (qn & 0x80000000u) pd = qn & 0x7fffffffu;
+      }
+      lb |= (uint64_t)los_march_c(X.S, X.mask, P.W16, pos_x(po), pos_y(po), pos_x(pd), pos_y(pd)) << (2 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      if (r0 + u >= NRAY) continue;
+      const int r = r0 + u, s = r / (2 * NPAIR), q = r % (2 * NPAIR);
+      const uint32_t f = (uint32_t)(fl >> (3 * u)) & 7u, l = (uint32_t)(lb >> (2 * u)) & 3u;
+      const int bit = (q & 1) * 16 + (q >> 1);
+      tR[s] |= ((f & 1u) && (l & 1u) ? 1u : 0u) << bit;
+      tC[s] |= ((f & 2u) && (l & 1u) ? 1u : 0u) << bit;
+      tW[s] |= ((f & 4u) && l == 3u ? 1u : 0u) << bit;
+    }
+  }
+  X.ptr_[0] = tR[0]; X.ptr_[1] = tR[1];
+  X.ptc[0] = tC[0]; X.ptc[1] = tC[1];
+  X.ptw[0] = tW[0]; X.ptw[1] = tW[1];
   X.pre = true;
 }
 
@@ -2708,7 +2829,9 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
     Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), emit ? S.mask2 : mask, E,
           r2col[lane], 0};
     unsigned long long tp[4] = {0, 0, 0, 0}, t0 = prof_now(S);  // LNW_PROF part totals
-    if constexpr (ST) {
+    if constexpr (ST && CW) {
+      pair_tables_t<NB, NR, true>(X);
+    } else if constexpr (ST) {
       if (P.los_mode != 1 && !(P.dbg_skip & 2048)) los_prefetch_t<NB, NR>(X);
     }
     tp[1] += prof_now(S) - t0;
@@ -2876,7 +2999,9 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
     if (sel >= 0) { a0 = sel; a1 = sel + 1; }
     else if (sel == LNW_OBS_BLUE) { a1 = nb; }
     else if (sel == LNW_OBS_RED) { a0 = nb; }
-    if constexpr (NB > 0) {
+    if constexpr (NB > 0 && CW) {
+      pair_tables_t<NB, NR, false>(X);
+    } else if constexpr (NB > 0) {
       if (P.los_mode != 1) los_prefetch_t<NB, NR>(X);
     }
     for (int a = a0; a < a1; a++) {
