@@ -1495,7 +1495,10 @@ __device__ inline void pair_tables_t(Ctx &X) {
     tr |= (uint32_t)COLB(c.type, NB + j) << (2 * j);
     radr |= (COLW(c.radar_cur, NB + j) == 1 ? 1u : 0u) << j;  // red's radar before the step
   }
-  // ray r: side s = r / (2*NPAIR); within a side q = (own*NOPP + opp)*2 + v
+  // ray r: side s = r / (2*NPAIR); within a side q = (own*NOPP + opp)*2 + v.
+  // The pair's ranges (rr2, re2) are computed on its v = 0 ray and reused by its
+  // v = 1 ray (the next one: chunks hold whole pairs)
+  int rr2 = 0, re2 = 0;
   auto ray = [&](int r, int &x1, int &y1, int &x2, int &y2, uint32_t &f) {
     const int s = r / (2 * NPAIR), q = r % (2 * NPAIR), v = q & 1, p = q >> 1;
     int o, d, ti, tj;
@@ -1519,11 +1522,14 @@ __device__ inline void pair_tables_t(Ctx &X) {
     }
     x1 = o >> 8; y1 = o & 255; x2 = d >> 8; y2 = d & 255;
     const int dx = x2 - x1, dy = y2 - y1, d2 = dx * dx + dy * dy;
-    f = 0;
-    if (need && d2 < X.r2max) {
+    if (v == 0) {
       const int rr = radar_r(P, duct, ti, tj), re = ew_r(P, duct, ti, tj);
-      f = (d2 < rr * rr ? 1u : 0u) | (d2 < 16 ? 2u : 0u) | (d2 < re * re && radj ? 4u : 0u);
+      rr2 = rr * rr;
+      re2 = re * re;
     }
+    f = 0;
+    if (need && d2 < X.r2max)
+      f = (d2 < rr2 ? 1u : 0u) | (d2 < 16 ? 2u : 0u) | (d2 < re2 && radj ? 4u : 0u);
   };
   uint32_t tR[2] = {0u, 0u}, tC[2] = {0u, 0u}, tW[2] = {0u, 0u};
   constexpr int NRAY = 4 * NPAIR;
