@@ -2633,7 +2633,7 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
                                          int nb, int A, const Neut &N, int (&ev)[8],
                                          const int (&hits)[2], int nbp, int nrp, int bsx, int bsy,
                                          int rsx, int rsy, Rng &rng, float *rew_b, float *rew_r,
-                                         int32_t *done_out, float *cog_out) {
+                                         int32_t *done_out, float *cog_out, bool quiet = false) {
   const long long E = P.E;
   const int nr = A - nb;
   double cog;
@@ -2665,11 +2665,14 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
     bool killed = (N.mask[side] >> (a - (side ? nb : 0))) & 1u;
     S.pos[ai] = COLW(c.pos_cur, a);
     S.radar[ai] = COLW(c.radar_cur, a);
+    S.steps[ai] = COLW(c.steps, a);
+    // a quiet step fires nothing, sinks nothing and leaves every target list
+    // empty (it was empty: env_quiet_t), so these four fields keep their values
+    if (quiet) continue;
     S.miss[ai] = COLB(c.miss_cur, a);
     S.mkind[ai] = COLB(c.mkind, a);
     S.alive[ai] = COLB(c.alive0, a) && !killed;
     S.tl_cnt[ai] = (uint16_t)COLW(c.tcnt, a);
-    S.steps[ai] = COLW(c.steps, a);
   }
 #pragma unroll
   for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
