@@ -2674,8 +2674,16 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
     S.alive[ai] = COLB(c.alive0, a) && !killed;
     S.tl_cnt[ai] = (uint16_t)COLW(c.tcnt, a);
   }
+  if (quiet) {  // the step counter, and the victory counters when the episode ends
+    S.envi[2 * E + env] = ev[2];
+    if (done == 0) {
+      S.envi[3 * E + env] = ev[3];
+      S.envi[4 * E + env] = ev[4];
+    }
+  } else {
 #pragma unroll
-  for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
+    for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
+  }
   if (do_reset) reset_env_dev(P, S, env, rng);
   S.rng[env] = rng.ctr;
   if (rng.err) S.err[env] |= rng.err;
