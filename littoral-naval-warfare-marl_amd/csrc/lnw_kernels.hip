@@ -2685,7 +2685,8 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
     for (int q = 0; q < 8; q++) S.envi[q * E + env] = ev[q];
   }
   if (do_reset) reset_env_dev(P, S, env, rng);
-  S.rng[env] = rng.ctr;
+  // a quiet step with a trained red draws nothing unless the env resets
+  if (!quiet || !P.trained_red || do_reset) S.rng[env] = rng.ctr;
   if (rng.err) S.err[env] |= rng.err;
 }
 

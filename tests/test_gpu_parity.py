@@ -92,6 +92,24 @@ def test_los_batch_vs_oracle_random(lib, grids):
         assert np.array_equal((o >> 1) & 1, los_batch(grids[gi], P, 70))
 
 
+def test_los_batch_large_grid_and_ragged(lib):
+    """lnw_los_batch beyond the LDS-staged size (G = 600: the 2-bit mask would
+    take 90 KB, so the one-lane HBM kernel runs), at the largest staged size
+    (G = 512: 64 KB of LDS) and with ray counts that leave a wave's queue
+    partly filled (1, 63, 1 025 rays), against the oracle."""
+    rng = np.random.default_rng(5)
+    for G, n in ((600, 20000), (512, 20000), (100, 1), (100, 63), (100, 1025)):
+        grid = rng.integers(0, 120, size=(G, G)).astype(np.uint8)
+        P = rng.integers(0, G, size=(n, 4)).astype(np.int16)
+        P[: n // 2, 2:] = np.clip(P[: n // 2, :2] + rng.integers(-40, 41, size=(n // 2, 2)), 0, G - 1)
+        out = torch.full((n,), 255, dtype=torch.uint8, device="cuda")
+        assert lib.lnw_los_batch(_p(_dev(grid)), G, _p(_dev(P)), n, 74, 70, _p(out), None) == 0
+        o = out.cpu().numpy()
+        assert np.array_equal(o & 1, los_batch(grid, P, 74)), G
+        assert np.array_equal((o >> 1) & 1, los_batch(grid, P, 70)), G
+        assert not np.any(o >> 2), G
+
+
 def test_astar_batch_golden(lib, grids):
     fx = load_fixture("astar.npz")
     for gi in (0, 1):
