@@ -42,16 +42,19 @@ CONFIG4 = dict(blue=["small"] * 8, red=["large"] * 8 + ["ls"] * 2, G=200, landin
                box=((20, 60), (80, 140)), rand_ls=[0] * 16 + [1, 1], envs=8192)
 
 
-def algorithmic_bytes(nb, nr):
+def algorithmic_bytes(nb, nr, quiet=False):
     """Minimum HBM bytes one env-step must move:
     actions in (f32), observations + rewards + done + cog out, and the SoA state
-    read and written once (26 B/agent + 52 B/env)."""
+    read once (26 B/agent + 52 B/env) and written back: all of it, or for a
+    quiet step (no pair in sensor range: reference spawns on the LOS-table path)
+    only what such a step changes — cell, radar and step counter per agent
+    (12 B) and the env's step counter (4 B)."""
     A = nb + nr
     act = A * 4 * 4
     obs = (nb * (4 * nb + 52) + nr * (4 * nr + 52)) * 4
     out = A * 4 + 4 + 4
     state = A * 26 + 52
-    return act + obs + out + 2 * state
+    return act + obs + out + state + (A * 12 + 4 if quiet else state)
 
 
 REF_LOS_CELLS = 10996  # SURVEY §8(d): Bresenham cells per 4v4 env-step, reference spawns
@@ -367,11 +370,11 @@ def cpu_baseline(seconds, threads):
                 single_thread_value=n1 / dt1)
 
 
-def line_entry(E, res, steps, nb=4, nr=4, desc=""):
+def line_entry(E, res, steps, nb=4, nr=4, desc="", quiet=False):
     """One secondary measurement: env-steps/s over the wall clock, the step
     kernel's mean time and its algorithmic bytes against the HBM roofline,
     and the device-counted ray-march / A* work per env-step."""
-    B = algorithmic_bytes(nb, nr)
+    B = algorithmic_bytes(nb, nr, quiet)
     el, km = res["elapsed"], res["kernel_ms"]
     ach = B * E / (km * 1e-3) / 1e9
     return dict(workload=desc, envs=E, env_steps_per_sec=E * steps / el, ms_per_step=el / steps * 1e3,
@@ -399,7 +402,8 @@ def secondary_lines(args):
             ("reference_los_work", 65536, "reference", 2, 0,
              "65 536 4v4 envs, reference spawns, plus the reference's LOS work: every own x "
              "opponent Bresenham ray of every get_obs marched in full (los_mode 2)")):
-        out[name] = line_entry(E, run_workload(E, 0, sp, lm, mm, K, W), K, desc=desc)
+        out[name] = line_entry(E, run_workload(E, 0, sp, lm, mm, K, W), K, desc=desc,
+                               quiet=sp == "reference" and lm == 0)
         log(name, out[name])
     E4 = CONFIG4["envs"]
     out["config4_8v10ls_g200"] = line_entry(
@@ -440,7 +444,7 @@ def main():
     err, episodes = (int(v) for v in dist.reduce_sum([err, episodes]))
     value = total * args.steps / elapsed
     nb, nr = (len(cfg["blue"]), len(cfg["red"])) if cfg else (4, 4)
-    B = algorithmic_bytes(nb, nr)
+    B = algorithmic_bytes(nb, nr, quiet=cfg is None and args.spawns == "reference" and args.los_mode == 0)
     achieved = B * E / (kms_mean * 1e-3) / 1e9
     traffic = measured_traffic(args, E)
     secondary = {}

@@ -46,6 +46,8 @@ def test_algorithmic_bytes():
     import bench
     # 4v4: actions 128 + obs 2176 + rewards/done/cog 40 + state 2*(8*26+52)
     assert bench.algorithmic_bytes(4, 4) == 128 + 2176 + 40 + 2 * (8 * 26 + 52)
+    # quiet steps write back cell, radar and step counter per agent and the env's step counter
+    assert bench.algorithmic_bytes(4, 4, quiet=True) == 128 + 2176 + 40 + (8 * 26 + 52) + (8 * 12 + 4)
 
 
 def test_packaged_grid_is_the_reference_grid():

@@ -102,7 +102,7 @@ def main():
     parts = key.split("_")
     E = int(parts[1][1:])
     nb, nr = (8, 10) if parts[0] == "config4" else (4, 4)
-    B = bench.algorithmic_bytes(nb, nr)
+    B = bench.algorithmic_bytes(nb, nr, quiet=parts[0] == "reference" and parts[2] == "los0")
     alg = B * E
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         fetch, write = pmc["FETCH_SIZE"] * 1024, pmc["WRITE_SIZE"] * 1024
