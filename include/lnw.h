@@ -223,9 +223,9 @@ int lnw_set_reward_dtype(lnw_handle *h, int32_t f64);
 /* ---- unit kernels (parity tests, standalone use) ------------------------ */
 /* LOS (radar thr = move_thr; EW thr): out[i] = bit0 radar clear | bit1 EW clear
  * for pairs[i] = (x1, y1, x2, y2), traced from (x1,y1) to (x2,y2); every cell of
- * the pairs must lie on the G x G grid (pairs_dev 8-byte aligned). Rays march
- * from the grid's 2-bit mask staged in LDS per workgroup (G <= 512), from HBM
- * above that. */
+ * the pairs must lie on the G x G grid. Rays march from the grid's 2-bit mask
+ * staged in LDS per workgroup (G <= 512, pairs_dev 8-byte aligned), else from
+ * HBM. */
 int lnw_los_batch(const uint8_t *grid_dev, int32_t G, const int16_t *pairs_dev, int64_t n,
                   int32_t move_thr, int32_t ew_thr, uint8_t *out_dev, void *stream);
 /* A*: plen[i] (-1 = None), kind[i] (0 goal, 1 timeout, 2 none), feasible[i]

@@ -4071,7 +4071,7 @@ int lnw_los_batch(const uint8_t *grid_dev, int32_t G, const int16_t *pairs_dev, 
   if (!grid_dev || !pairs_dev || !out_dev) return fail(LNW_EINVAL, "null argument");
   if (n <= 0) return 0;
   const size_t lds = (size_t)G * ((G + 15) / 16) * 4;
-  if (lds <= 64 * 1024) {
+  if (lds <= 64 * 1024 && ((uintptr_t)pairs_dev & 7) == 0) {  // (the LDS kernel reads a pair as 8 bytes)
     const long long per_block = (long long)(LB_THREADS / WAVE) * LB_RAYS_PER_WAVE;
     los_batch_kernel<<<(unsigned)((n + per_block - 1) / per_block), LB_THREADS, lds, (hipStream_t)stream>>>(
         grid_dev, G, pairs_dev, n, move_thr, ew_thr, out_dev);

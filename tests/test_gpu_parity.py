@@ -108,6 +108,17 @@ def test_los_batch_large_grid_and_ragged(lib):
         assert np.array_equal(o & 1, los_batch(grid, P, 74)), G
         assert np.array_equal((o >> 1) & 1, los_batch(grid, P, 70)), G
         assert not np.any(o >> 2), G
+    # a pairs buffer 2 bytes into its allocation (not 8-byte aligned: the HBM kernel)
+    G, n = 100, 5000
+    grid = rng.integers(0, 120, size=(G, G)).astype(np.uint8)
+    P = rng.integers(0, G, size=(n, 4)).astype(np.int16)
+    buf = torch.zeros(4 * n + 1, dtype=torch.int16, device="cuda")
+    buf[1:] = torch.from_numpy(P.reshape(-1)).cuda()
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    assert lib.lnw_los_batch(_p(_dev(grid)), G, _p(buf[1:]), n, 74, 70, _p(out), None) == 0
+    o = out.cpu().numpy()
+    assert np.array_equal(o & 1, los_batch(grid, P, 74))
+    assert np.array_equal((o >> 1) & 1, los_batch(grid, P, 70))
 
 
 def test_astar_batch_golden(lib, grids):
