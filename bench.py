@@ -293,7 +293,7 @@ def mappo_rollout(total=32768, T=40, reps=3):
     critic = BatchedCritic(g.Db * g.nb).cuda()
     gen = torch.Generator(device="cuda").manual_seed(5 + rank)
     g.set_variant(True)  # scripted red closes in: contact most steps
-    r = Rollout(g, actor, critic, steps=T, noise=0.05)
+    r = Rollout(g, actor, critic, steps=T, noise=0.05, seed=5)  # fused HIP policy kernels, keyed by global row
     g.reset(positions=REF_BLUE + REF_RED)
     r.run(generator=gen)
     torch.cuda.synchronize()
@@ -311,7 +311,7 @@ def mappo_rollout(total=32768, T=40, reps=3):
 
     dt = timed(lambda: r.run(generator=gen))
     # the same rollout replayed from a HIP graph (Rollout.capture): no host work
-    # between the ~30 kernels of a step
+    # between the four launches of a step
     g.reset(positions=REF_BLUE + REF_RED)
     r.capture(generator=gen)
     torch.cuda.synchronize()
@@ -320,8 +320,10 @@ def mappo_rollout(total=32768, T=40, reps=3):
     return dict(env_steps_per_sec=total * T / dtg, ms_per_rollout=dtg * 1e3,
                 eager_env_steps_per_sec=total * T / dt, eager_ms_per_rollout=dt * 1e3,
                 envs=total, envs_per_gpu=E, n_gpus=world, steps=T,
-                policy="batched actor (network.py MLP) + critic (Value), fp32; HIP-graph replay "
-                       "(eager loop alongside); max over ranks")
+                policy="fused HIP policy step (lnw_policy_act: conv head + MLP + keyed sample + "
+                       "log-prob + action array; lnw_rollout_post: critic + rewards), fp32; per step "
+                       "observe, policy, step, post = 4 launches; HIP-graph replay (eager loop "
+                       "alongside); max over ranks")
 
 
 def cpu_baseline(seconds, threads):

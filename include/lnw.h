@@ -32,7 +32,9 @@
  *    the err-flags array (LNW_ERRF_*).
  *  - A handle is not thread-safe; use one handle per device (per process).
  *
- * Layouts (E = n_envs, nb/nr = blue/red slots, A = nb+nr, D_side = 4*n_side+52):
+ * Layouts (E = n_envs, nb/nr = blue/red slots, A = nb+nr, D_side = 4*n_side+52,
+ * or 4*n_side+28 for a side of medium ships: game.py:609-610 sizes a side's rows
+ * by its fastest ship, (2*speed+1)^2 window cells):
  *  actions   [E][A][4]  f32 or f64 (continuous), or [E][A][4] i32 (discrete:
  *                       radar, salvo, move-index 0..49, unused) — mutated in
  *                       place where the reference mutates it (game.py:379)
@@ -52,7 +54,7 @@
 extern "C" {
 #endif
 
-#define LNW_ABI_VERSION 3
+#define LNW_ABI_VERSION 4
 
 /* status codes */
 #define LNW_OK 0
@@ -62,10 +64,12 @@ extern "C" {
 #define LNW_ESTATE (-4)
 #define LNW_EUNSUPPORTED (-5)
 
-/* ship types (Combatant "small"/"large", LandingShip "ls") */
+/* ship types (Combatant "small"/"large"/"medium", LandingShip "ls";
+ * combatant.py:60-88, landingship.py:61-92, game.py:184-212) */
 #define LNW_SMALL 0
 #define LNW_LARGE 1
 #define LNW_LS 2
+#define LNW_MEDIUM 3   /* speed 2, 8 missiles, mast 30, rcs 1, 5x5 observation window */
 
 /* action dtypes / per-row value kinds (NumPy NEP 50 semantics) */
 #define LNW_ACT_F32 0      /* whole buffer float32 (np.float32 rows)            */
@@ -115,7 +119,10 @@ typedef struct lnw_params {
 } lnw_params;
 
 /* Spawn description used by lnw_reset and by in-kernel auto-reset.
- * types[A]: LNW_SMALL/LARGE/LS; pos[A][2]: spawn cell; rand_ls[A] != 0 draws the
+ * types[A]: LNW_SMALL/LARGE/LS/MEDIUM (medium ships only as a whole side: the
+ * reference's row assignment raises for a medium ship beside speed-3 ships,
+ * game.py:344 / 381, so lnw_reset refuses that with LNW_EUNSUPPORTED);
+ * pos[A][2]: spawn cell; rand_ls[A] != 0 draws the
  * cell with random.randint(98,99), random.randint(48,56) (game.py:589).
  * If box_lo/box_hi are set (box_hi[0] > box_lo[0]) every agent instead spawns on
  * a random water cell of that box (a build-side "melee" scenario, drawn from a
@@ -184,6 +191,32 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
 
 /* Device pointer and byte size of one state field (valid until lnw_destroy). */
 int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbytes);
+
+/* Whole-state snapshot (SURVEY.md §8(b) lnw_get_state / lnw_set_state; the
+ * reference has no counterpart: its state is the Game object itself, and
+ * checkpointing it means pickling that object). A snapshot holds every state
+ * field above, the spawn spec and per-env spawn cells the in-kernel auto-reset
+ * reads, the RNG mode and seed, and a header naming the handle's shape and a
+ * hash of its terrain. lnw_set_state restores it into any handle of the same
+ * shape (envs, team sizes, grid) and terrain — the same one later, or a fresh
+ * one — after which stepping continues exactly as the saved handle would have.
+ * A tape-mode snapshot restores the tape cursors only: bind the same tape with
+ * lnw_set_rng first. dst / src: host or device memory of at least
+ * lnw_state_bytes(h) bytes. Both wait for `stream` and copy synchronously. */
+int64_t lnw_state_bytes(lnw_handle *h);
+int lnw_get_state(lnw_handle *h, void *dst, int64_t nbytes, void *stream);
+int lnw_set_state(lnw_handle *h, const void *src, int64_t nbytes, void *stream);
+
+/* The step kernel the last lnw_step launched (build-side launch shape, no
+ * reference counterpart; tests use it to know which code path they checked). */
+#define LNW_KERNEL_NONE 0
+#define LNW_KERNEL_GENERIC 1       /* one lane per env, runtime team sizes         */
+#define LNW_KERNEL_TEAM 2          /* 2v2/3v3/4v4, one unit (<= 64 envs) per workgroup */
+#define LNW_KERNEL_TEAM_CONTACT 3  /* the same, contact variant (lnw_set_variant)  */
+#define LNW_KERNEL_UNITS 4         /* 4v4 headline: four 64-env units per workgroup */
+#define LNW_KERNEL_GROUP 5         /* runtime team sizes, 16 lanes per env         */
+#define LNW_KERNEL_REFLOS 6        /* los_mode 2 (the reference's LOS work)        */
+int lnw_step_kernel(lnw_handle *h);
 /* Target-list capacity T per agent (= max(nb,nr) + max(nb,nr)^2, never overflows). */
 int lnw_tlist_cap(lnw_handle *h);
 /* Environments per workgroup of the step / observe launches (build-side launch
@@ -208,8 +241,10 @@ int lnw_set_variant(lnw_handle *h, int32_t contact);
  * (queries outside the LOS table, or every query with los_mode = 1), to [1] the
  * Bresenham cells those rays visit (combatant.py:411-456) and to [2] the A*
  * searches they run (targets outside the move table, or move_mode = 1;
- * combatant.py:289-408), to [3] the EW bearings the contact variant evaluates
- * in wave-pooled rounds (get_obs calls whose busiest lane has more than two).
+ * combatant.py:289-408), to [3] the EW bearings evaluated pooled across lanes:
+ * by the contact variant in wave-pooled rounds (get_obs calls whose busiest
+ * lane has more than two), by the group kernel (runtime team sizes) every
+ * bearing of an opponent that gets a fix (spread over the env's 16 lanes).
  * counters_dev: [4] uint64 device array, or NULL to unbind. Costs one uniform
  * branch per march / search / pooled get_obs while unbound. */
 int lnw_set_counters(lnw_handle *h, uint64_t *counters_dev);
@@ -242,7 +277,12 @@ int lnw_move_batch(lnw_handle *h, const int8_t *types_dev, const int16_t *pos_de
  * targets within +-4) or the A* replica. start must lie inside the grid. */
 int lnw_path_query(lnw_handle *h, const int8_t *types_dev, const int16_t *start_dev,
                    const int16_t *target_dev, int64_t n, uint8_t *out_dev, void *stream);
-/* The handle's LOS query (table or march per params.los_mode). */
+/* The handle's LOS query (table or march per params.los_mode). Together with
+ * params.los_mode = 1 (every query marched) and 2 (the reference's full
+ * own x opponent LOS work inside the step), this is what SURVEY.md §8(b)'s
+ * lnw_debug_los (the full unpruned LOS matrix) was to provide: any pair set
+ * can be queried through the step's own LOS path, bit-exact with
+ * check_line_of_sight (combatant.py:436-456). */
 int lnw_los_query(lnw_handle *h, const int16_t *pairs_dev, int64_t n, uint8_t *out_dev,
                   void *stream);
 
@@ -290,6 +330,68 @@ int lnw_set_analytics(lnw_handle *h, const lnw_analytics *a);
  * statistics (the reference's training-mode one-state calls), 1: running. */
 int lnw_actor_features(const float *params_dev, int32_t obs_dim, const float *obs_dev, int64_t B,
                        int32_t bn_running, float *out_dev /* [B][n_in] */, void *stream);
+
+/* ---- fused rollout step of the MAPPO caller -----
+ * lnw_policy_act replaces, per step and side, the reference rollout's actor
+ * calls (ppo.py:497-575: MLP.forward per live ship, network.py:70-115, or
+ * MLP.get_dist :117-152 for given actions) and the assembly of the action
+ * array (ppo.py:515-577), for every env at once: conv head + LayerNorm + tanh
+ * MLP + Normal heads, a keyed Philox sample clamped to [0, 1] (+ N(0, noise)),
+ * its log-probability, then the f64 rows lnw_step takes (sunk ships 0), the
+ * rollout buffer rows, scripted red rows (red_steps*.csv, ppo.py:560-566) and
+ * the rows' value kinds (np.asarray of the step's rows, ppo.py:577).
+ * params: BatchedActor.packed_policy() (lnw/rollout.py). One launch. */
+typedef struct lnw_policy_args {
+  const float *obs;            /* [E][n][D] this side's observation rows (16-B aligned) */
+  int64_t E;
+  int32_t n, D, own0, A;       /* ships of the side, row length, first agent slot, agents per env */
+  const float *params;
+  int32_t bn_running;          /* 0: per-row BatchNorm statistics (training-mode batch-1 calls) */
+  int32_t forced;              /* 1: log-probabilities of forced_act (get_dist), no sampling */
+  const float *forced_act;     /* rows of 4 floats: env e ship i at [e * fa_env_stride + 4 i] */
+  int64_t fa_env_stride;
+  float noise;                 /* > 0: + noise * N(0, 1) before the clamp */
+  uint64_t seed;               /* keyed draws: Philox(seed) at slot (call * T + t) * 4 + which */
+  const int64_t *call_dev;     /* rollout index, read on the device (NULL = 0) */
+  int32_t T, t, which;
+  int64_t row_base;            /* global id of row 0 (env_id_base * n) */
+  const uint8_t *alive;        /* [A][E] the handle's LNW_F_ALIVE field */
+  const uint8_t *live;         /* [E] episode still running (NULL: all) */
+  float *obs_out;              /* NULL, or rollout rows: env e at obs_out + e * obs_env_stride */
+  int64_t obs_env_stride;
+  float *act_out, *logp_out;   /* NULL, or rollout rows of 4: env e ship i at e * act_env_stride + 4 i */
+  int64_t act_env_stride;
+  double *full;                /* [E][A][4] action array of lnw_step (this side's rows), or NULL */
+  const double *script;        /* NULL, or scripted rows [script_n][script_steps][4] */
+  int32_t script_n, script_steps, script_own0, script_cnt;
+  uint8_t *kinds;              /* NULL, or [E][A] row kinds for lnw_step */
+  int32_t kinds_f32_all_alive; /* 1: LNW_KIND_F32 rows when every ship is alive, else F64 */
+  uint8_t *f32_out;            /* NULL, or env e at f32_out[e * f32_env_stride]: the rows are F32 */
+  int64_t f32_env_stride;
+} lnw_policy_args;
+int lnw_policy_act(const lnw_policy_args *args, void *stream);
+
+/* After lnw_step: the rollout's bookkeeping of step t (ppo.py:598-641) and the
+ * critic (Value, network.py:154-172) on the rows the actor saw: value (0 after
+ * the episode ended), rewards (ditto), running flag, and live &= done != 0. */
+typedef struct lnw_rollout_post_args {
+  const float *obs;            /* rollout rows of step t: env e at obs + e * obs_env_stride, [n][D] */
+  int64_t obs_env_stride, E;
+  int32_t n, D;
+  const float *critic;         /* BatchedCritic.packed(), or NULL (no value) */
+  float *val;                  /* env e at val[e * val_env_stride] */
+  int64_t val_env_stride;
+  const void *rew;             /* [E][n_rew] lnw_step rewards (float32, or float64 if rew_f64) */
+  int32_t rew_f64, n_rew;
+  double *rew_out;             /* NULL, or env e at rew_out + e * rew_env_stride */
+  int64_t rew_env_stride;
+  const int32_t *done;         /* [E] lnw_step done */
+  uint8_t *live;               /* [E] in/out */
+  uint8_t *running;            /* NULL, or env e at running[e * running_env_stride] */
+  int64_t running_env_stride;
+  int32_t stop_at_done;        /* mask values / rewards after the episode ended, update live */
+} lnw_rollout_post_args;
+int lnw_rollout_post(const lnw_rollout_post_args *args, void *stream);
 
 /* Host-side constants the kernels use (for tests): hit probability tables
  * 1-(1-p)^n for p in {0.45, 0.63}, n = 0..8, in float64 and float32. */

@@ -39,6 +39,13 @@ constexpr float LN_EPS = 1e-5f;
 
 extern __shared__ float actor_lds[];
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+// read-only parameters through the constant address space: wave-uniform
+// indices then become scalar loads (s_load / s_buffer_load) into SGPRs, one
+// load per 16 weights for the whole wave, instead of per-lane vector loads
+typedef const __attribute__((address_space(4))) float cfloat;
+
 // BatchNorm of one channel's n values: own statistics (biased variance) or
 // running ones, then the affine, then ReLU.
 template <int N>
@@ -65,6 +72,101 @@ __device__ inline void bn_relu(float (&v)[N], const float *w, const float *b, co
 
 constexpr int CH_THREADS = 256;
 
+// The conv head of one row (network.py:70-82): conv 1->5 over the 7x7 window
+// x[0..48] -> BN -> ReLU -> 2x2 pool, conv 5->8 -> BN -> ReLU -> pool, folded
+// into the linear 8->12 (h). P: packed parameters in LDS (broadcast reads);
+// pool1: this workgroup's [45][CH_THREADS] parking area, t: the thread's column.
+__device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pool1, int t,
+                                              bool running, float (&h)[12]) {
+  float win[WIN];
+#pragma unroll
+  for (int i = 0; i < WIN; i++) win[i] = x[i];
+  // conv1 (1 -> 5, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (7x7 -> 3x3),
+  // one channel at a time (rolled: 49 outputs live)
+#pragma unroll 1
+  for (int c = 0; c < 5; c++) {
+    float v[49];
+    const float *w = P + C1W + c * 9;
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+        float s = P[C1B + c];
+#pragma unroll
+        for (int ki = 0; ki < 3; ki++)
+#pragma unroll
+          for (int kj = 0; kj < 3; kj++) {
+            const int ii = i + ki - 1, jj = j + kj - 1;
+            if (ii >= 0 && ii < 7 && jj >= 0 && jj < 7) s += w[ki * 3 + kj] * win[ii * 7 + jj];
+          }
+        v[i * 7 + j] = s;
+      }
+    bn_relu<49>(v, P + B1W, P + B1B, P + B1M, P + B1V, c, running);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const int r0 = 2 * i, c0 = 2 * j;
+        pool1[(c * 9 + i * 3 + j) * CH_THREADS + t] =
+            fmaxf(fmaxf(v[r0 * 7 + c0], v[r0 * 7 + c0 + 1]),
+                  fmaxf(v[(r0 + 1) * 7 + c0], v[(r0 + 1) * 7 + c0 + 1]));
+      }
+  }
+  float p1[45];
+#pragma unroll
+  for (int k = 0; k < 45; k++) p1[k] = pool1[k * CH_THREADS + t];
+  // conv2 (5 -> 8, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (3x3 -> 1x1),
+  // folded straight into the linear 8 -> 12 (convhead)
+#pragma unroll
+  for (int k = 0; k < 12; k++) h[k] = P[HB + k];
+#pragma unroll 1
+  for (int co = 0; co < 8; co++) {
+    float v[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        float s = P[C2B + co];
+#pragma unroll
+        for (int ci = 0; ci < 5; ci++) {
+          const float *w = P + C2W + (co * 5 + ci) * 9;
+#pragma unroll
+          for (int ki = 0; ki < 3; ki++)
+#pragma unroll
+            for (int kj = 0; kj < 3; kj++) {
+              const int ii = i + ki - 1, jj = j + kj - 1;
+              if (ii >= 0 && ii < 3 && jj >= 0 && jj < 3)
+                s += w[ki * 3 + kj] * p1[ci * 9 + ii * 3 + jj];
+            }
+        }
+        v[i * 3 + j] = s;
+      }
+    bn_relu<9>(v, P + B2W, P + B2B, P + B2M, P + B2V, co, running);
+    const float f = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[3], v[4]));
+#pragma unroll
+    for (int k = 0; k < 12; k++) h[k] += P[HW + k * 8 + co] * f;
+  }
+}
+
+// LayerNorm over [h, x[49:]] (biased variance) with its affine, into u[0..n_in)
+template <int NI>
+__device__ __forceinline__ void layer_norm_row(const float *P, const float *x, int n_in, const float (&h)[12],
+                                               float (&u)[NI]) {
+#pragma unroll
+  for (int k = 0; k < NI; k++) u[k] = k < 12 ? h[k < 12 ? k : 0] : (k < n_in ? x[WIN + k - 12] : 0.f);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NI; k++) s += k < n_in ? u[k] : 0.f;
+  const float mean = s / (float)n_in;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NI; k++) q += k < n_in ? (u[k] - mean) * (u[k] - mean) : 0.f;
+  const float inv = 1.0f / sqrtf(q / (float)n_in + LN_EPS);
+  const float *lw = P + CONV_PARAMS, *lb = P + CONV_PARAMS + n_in;
+#pragma unroll
+  for (int k = 0; k < NI; k++) u[k] = k < n_in ? (u[k] - mean) * inv * lw[k] + lb[k] : 0.f;
+}
+
 __global__ __launch_bounds__(CH_THREADS, 2) void features_kernel(const float *params, int obs_dim,
                                                               const float *obs, long long B,
                                                               int bn_running, float *out) {
@@ -79,93 +181,326 @@ __global__ __launch_bounds__(CH_THREADS, 2) void features_kernel(const float *pa
   for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < B;
        row += (long long)gridDim.x * blockDim.x) {
     const float *x = obs + row * obs_dim;
-    float win[WIN];
-#pragma unroll
-    for (int i = 0; i < WIN; i++) win[i] = x[i];
-    // conv1 (1 -> 5, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (7x7 -> 3x3),
-    // one channel at a time (rolled: 49 outputs live)
-#pragma unroll 1
-    for (int c = 0; c < 5; c++) {
-      float v[49];
-      const float *w = P + C1W + c * 9;
-#pragma unroll
-      for (int i = 0; i < 7; i++)
-#pragma unroll
-        for (int j = 0; j < 7; j++) {
-          float s = P[C1B + c];
-#pragma unroll
-          for (int ki = 0; ki < 3; ki++)
-#pragma unroll
-            for (int kj = 0; kj < 3; kj++) {
-              const int ii = i + ki - 1, jj = j + kj - 1;
-              if (ii >= 0 && ii < 7 && jj >= 0 && jj < 7) s += w[ki * 3 + kj] * win[ii * 7 + jj];
-            }
-          v[i * 7 + j] = s;
-        }
-      bn_relu<49>(v, P + B1W, P + B1B, P + B1M, P + B1V, c, running);
-#pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-          const int r0 = 2 * i, c0 = 2 * j;
-          pool1[(c * 9 + i * 3 + j) * CH_THREADS + t] =
-              fmaxf(fmaxf(v[r0 * 7 + c0], v[r0 * 7 + c0 + 1]),
-                    fmaxf(v[(r0 + 1) * 7 + c0], v[(r0 + 1) * 7 + c0 + 1]));
-        }
-    }
-    float p1[45];
-#pragma unroll
-    for (int k = 0; k < 45; k++) p1[k] = pool1[k * CH_THREADS + t];
-    // conv2 (5 -> 8, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (3x3 -> 1x1),
-    // folded straight into the linear 8 -> 12 (convhead)
     float h[12];
-#pragma unroll
-    for (int k = 0; k < 12; k++) h[k] = P[HB + k];
-#pragma unroll 1
-    for (int co = 0; co < 8; co++) {
-      float v[9];
-#pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-          float s = P[C2B + co];
-#pragma unroll
-          for (int ci = 0; ci < 5; ci++) {
-            const float *w = P + C2W + (co * 5 + ci) * 9;
-#pragma unroll
-            for (int ki = 0; ki < 3; ki++)
-#pragma unroll
-              for (int kj = 0; kj < 3; kj++) {
-                const int ii = i + ki - 1, jj = j + kj - 1;
-                if (ii >= 0 && ii < 3 && jj >= 0 && jj < 3)
-                  s += w[ki * 3 + kj] * p1[ci * 9 + ii * 3 + jj];
-              }
-          }
-          v[i * 3 + j] = s;
-        }
-      bn_relu<9>(v, P + B2W, P + B2B, P + B2M, P + B2V, co, running);
-      const float f = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[3], v[4]));
-#pragma unroll
-      for (int k = 0; k < 12; k++) h[k] += P[HW + k * 8 + co] * f;
-    }
-    // LayerNorm over [h, x[49:]] (biased variance), affine
+    conv_head_row(P, x, pool1, t, running, h);
     float u[MAX_IN];
-#pragma unroll
-    for (int k = 0; k < MAX_IN; k++) u[k] = k < 12 ? h[k < 12 ? k : 0] : (k < n_in ? x[WIN + k - 12] : 0.f);
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAX_IN; k++) s += k < n_in ? u[k] : 0.f;
-    const float mean = s / (float)n_in;
-    float q = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAX_IN; k++) q += k < n_in ? (u[k] - mean) * (u[k] - mean) : 0.f;
-    const float inv = 1.0f / sqrtf(q / (float)n_in + LN_EPS);
+    layer_norm_row<MAX_IN>(P, x, n_in, h, u);
     float *o = out + row * n_in;
-    const float *lw = P + CONV_PARAMS, *lb = P + CONV_PARAMS + n_in;
 #pragma unroll
     for (int k = 0; k < MAX_IN; k++)
-      if (k < n_in) o[k] = (u[k] - mean) * inv * lw[k] + lb[k];
+      if (k < n_in) o[k] = u[k];
   }
+}
+
+// ---------------------------------------------------------------------------
+// Fused policy step (lnw_policy_act): for every row of one side's observation
+// block, the whole reference actor forward (network.py:70-115 / get_dist
+// :117-152) and what the MAPPO rollout does with it (ppo.py:497-577) in one
+// launch, one thread per row:
+//   conv head + LayerNorm (as features_kernel), then fc1 64 / fc2 64 / fc3 32
+//   tanh layers and the normal / log-std heads with weights read as wave-
+//   uniform scalar loads (every lane of the wave uses the same weight), fp32
+//   FMA;
+//   NaN heads -> N(0, 1) for the row (the reference returns None there);
+//   sample: N(mean, std) from keyed Philox normals (+ N(0, noise)), clamped to
+//   [0, 1], and its log-probability; or, forced, the log-probability of given
+//   actions (get_dist);
+//   outputs: the f64 action rows of lnw_step (sunk ships 0), the rollout's
+//   action / log-probability rows (0 after the episode ended) and the
+//   observation copy for the rollout buffer; the lane of ship 0 also writes its
+//   env's scripted red rows (red_steps*.csv, ppo.py:560-566) and the action
+//   array's row kinds (np.asarray, ppo.py:577).
+// Keyed draws (keyed_normal in lnw/rollout.py): uniform k of global row r at
+// Philox counter (slot << 40) / 4 + 2 r (+1), slot = (call * T + t) * 4 + which;
+// eps = sqrt(-2 log1p(-u_c)) cos(2 pi u_{4+c}); `call` is read from device
+// memory so a replayed graph draws fresh values every rollout.
+// ---------------------------------------------------------------------------
+constexpr int FC1 = 64, FC2 = 64, FC3 = 32, NOUT = 4;
+
+struct PolicyArgs {
+  lnw_policy_args a;
+  int n_in;
+  int off_w1, off_b1, off_w2, off_b2, off_w3, off_b3, off_wm, off_ws;  // packed MLP offsets (floats)
+};
+
+__device__ __forceinline__ void philox_u8(unsigned long long seed, unsigned long long ctr0, float (&u)[8]) {
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const unsigned long long ctr = ctr0 + (unsigned long long)b;
+    uint32_t o[4] = {(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x243F6A88u, 0x85A308D3u};
+    philox10(o, (uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int k = 0; k < 4; k++) u[4 * b + k] = (float)(o[k] >> 8) * 5.9604644775390625e-08f;
+  }
+}
+
+// standard normals of (slot, global row): keyed_normal's construction
+__device__ __forceinline__ void keyed_eps(unsigned long long seed, unsigned long long slot, long long grow,
+                                          float (&eps)[NOUT]) {
+  float u[8];
+  philox_u8(seed, (slot << 38) + (unsigned long long)grow * 2ull, u);
+#pragma unroll
+  for (int c = 0; c < NOUT; c++) eps[c] = sqrtf(-2.0f * log1pf(-u[c])) * cosf(6.283185307179586f * u[4 + c]);
+}
+
+// tanh(W x + b) of one row for a layer of NO outputs, W row-major [NO][NI]
+// (torch's nn.Linear layout; fc1 zero-padded to NI columns), x in registers,
+// outputs to the thread's LDS column col[o * CH_THREADS]
+template <int NI, int NO>
+__device__ __forceinline__ void dense_layer(cfloat *W, cfloat *b, const float (&x)[NI], float *col) {
+#pragma unroll 1
+  for (int o = 0; o < NO; o += 2) {
+    float a0 = b[o], a1 = b[o + 1];
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+      a0 = fmaf(W[o * NI + k], x[k], a0);
+      a1 = fmaf(W[(o + 1) * NI + k], x[k], a1);
+    }
+    col[o * CH_THREADS] = tanhf(a0);
+    col[(o + 1) * CH_THREADS] = tanhf(a1);
+  }
+}
+
+template <int NI>
+__global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa) {
+  const lnw_policy_args &a = pa.a;
+  const int n_in = pa.n_in;
+  const int n_par = CONV_PARAMS + 2 * n_in;
+  float *P = actor_lds;                // [n_par] conv head + LayerNorm parameters
+  float *pool1 = actor_lds + n_par;    // [64][CH_THREADS]: conv1 maps, then the MLP layer columns
+  for (int i = threadIdx.x; i < n_par; i += blockDim.x) P[i] = a.params[i];
+  const int n = a.n, D = a.D;
+  const long long rows = a.E * n;
+  const long long r0 = (long long)blockIdx.x * CH_THREADS;
+  // observation copy for the rollout buffer: the block's rows, float4 chunks
+  if (a.obs_out) {
+    const int D4 = D >> 2;
+    const long long nr = rows - r0 < CH_THREADS ? rows - r0 : CH_THREADS;
+    const f32x4 *src = (const f32x4 *)(a.obs + r0 * D);
+    for (int q = threadIdx.x; q < nr * D4; q += CH_THREADS) {
+      const long long r = r0 + q / D4;
+      const int c4 = q - (q / D4) * D4;
+      const long long e = r / n;
+      const int i = (int)(r - e * n);
+      f32x4 v = src[q];
+      if (a.live && !a.live[e]) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      *(f32x4 *)(a.obs_out + e * a.obs_env_stride + (long long)i * D + 4 * c4) = v;
+    }
+  }
+  __syncthreads();
+  const long long r = r0 + threadIdx.x;
+  if (r >= rows) return;
+  const long long e = r / n;
+  const int i = (int)(r - e * n);
+  const long long E = a.E;
+  const bool alive = a.alive[(long long)(a.own0 + i) * E + e] != 0;
+  const bool live = !a.live || a.live[e] != 0;
+  // ---- env-level side work by the lane of ship 0 ---------------------------
+  if (i == 0) {
+    if (a.script) {  // scripted rows: profile j for red ship j < script_n, zeros past the table
+      for (int j = 0; j < a.script_cnt; j++) {
+        const int ag = a.script_own0 + j;
+        const bool al = a.alive[(long long)ag * E + e] != 0;
+        const bool has = j < a.script_n && a.t < a.script_steps;
+        f64x4 v = {0.0, 0.0, 0.0, 0.0};
+        if (al && has) v = *(const f64x4 *)(a.script + ((long long)j * a.script_steps + a.t) * 4);
+        *(f64x4 *)(a.full + (e * a.A + ag) * 4) = v;
+      }
+    }
+    if (a.kinds) {
+      bool all = true;
+      for (int ag = 0; ag < a.A; ag++) all = all && a.alive[(long long)ag * E + e] != 0;
+      const uint8_t k = (a.kinds_f32_all_alive && all) ? (uint8_t)LNW_KIND_F32 : (uint8_t)LNW_KIND_F64;
+      for (int ag = 0; ag < a.A; ag++) a.kinds[e * a.A + ag] = k;
+      if (a.f32_out) a.f32_out[e * a.f32_env_stride] = k == LNW_KIND_F32 ? 1 : 0;
+    }
+  }
+  // ---- actor forward --------------------------------------------------------
+  const float *x = a.obs + r * D;
+  float h[12];
+  conv_head_row(P, x, pool1, threadIdx.x, a.bn_running != 0, h);
+  float u[NI];
+  layer_norm_row<NI>(P, x, n_in, h, u);
+  // MLP: each layer's outputs two at a time (independent FMA chains over the
+  // inputs, held in registers under static indices) with the weights of those
+  // two rows as scalar loads; outputs go to the thread's LDS column (the conv
+  // scratch, dead now) and are read back as the next layer's register inputs.
+  // (Fully unrolled layers had the compiler hoist thousands of scalar weight
+  // loads and spill them.)
+  cfloat *W = (cfloat *)a.params;
+  float *col = pool1 + threadIdx.x;  // [FC1][CH_THREADS]
+  dense_layer<NI, FC1>(W + pa.off_w1, W + pa.off_b1, u, col);
+  float h1[FC1];
+#pragma unroll
+  for (int k = 0; k < FC1; k++) h1[k] = col[k * CH_THREADS];
+  dense_layer<FC1, FC2>(W + pa.off_w2, W + pa.off_b2, h1, col);
+  float h2[FC2];
+#pragma unroll
+  for (int k = 0; k < FC2; k++) h2[k] = col[k * CH_THREADS];
+  dense_layer<FC2, FC3>(W + pa.off_w3, W + pa.off_b3, h2, col);
+  float h3[FC3];
+#pragma unroll
+  for (int k = 0; k < FC3; k++) h3[k] = col[k * CH_THREADS];
+  float mean[NOUT], lsd[NOUT];
+#pragma unroll
+  for (int o = 0; o < NOUT; o++) {
+    float m = 0.f, l = 0.f;
+#pragma unroll
+    for (int k = 0; k < FC3; k++) {
+      m = fmaf(W[pa.off_wm + o * FC3 + k], h3[k], m);
+      l = fmaf(W[pa.off_ws + o * FC3 + k], h3[k], l);
+    }
+    mean[o] = m;
+    lsd[o] = l;
+  }
+  float std_[NOUT];
+  bool ok = true;
+#pragma unroll
+  for (int o = 0; o < NOUT; o++) {
+    mean[o] = tanhf(mean[o]);
+    std_[o] = expf(lsd[o]);
+    ok = ok && !isnan(mean[o]) && !isnan(std_[o]);
+  }
+  // ---- sample / forced actions and log-probabilities -----------------------
+  float act[NOUT], lp[NOUT];
+  if (a.forced) {  // MLP.get_dist (network.py:117-152): no NaN guard
+    const float *fa = a.forced_act + e * a.fa_env_stride + 4 * i;
+#pragma unroll
+    for (int o = 0; o < NOUT; o++) act[o] = fa[o];
+  } else {
+    if (!ok) {
+#pragma unroll
+      for (int o = 0; o < NOUT; o++) { mean[o] = 0.f; std_[o] = 1.f; }
+    }
+    const unsigned long long call = a.call_dev ? (unsigned long long)*a.call_dev : 0ull;
+    const unsigned long long slot = (call * (unsigned long long)a.T + (unsigned long long)a.t) * 4ull;
+    const long long grow = a.row_base + r;
+    float eps[NOUT];
+    keyed_eps(a.seed, slot + (unsigned long long)a.which, grow, eps);
+#pragma unroll
+    for (int o = 0; o < NOUT; o++) act[o] = mean[o] + std_[o] * eps[o];
+    if (a.noise > 0.f) {
+      float ne[NOUT];
+      keyed_eps(a.seed, slot + (unsigned long long)a.which + 1ull, grow, ne);
+#pragma unroll
+      for (int o = 0; o < NOUT; o++) act[o] = act[o] + a.noise * ne[o];
+    }
+#pragma unroll
+    for (int o = 0; o < NOUT; o++) act[o] = fminf(fmaxf(act[o], 0.f), 1.f);
+  }
+  // Normal.log_prob (torch.distributions): -((x - m)^2) / (2 var) - log(std) - log(sqrt(2 pi))
+#pragma unroll
+  for (int o = 0; o < NOUT; o++) {
+    const float d = act[o] - mean[o];
+    const float var = std_[o] * std_[o];
+    lp[o] = -(d * d) / (2.0f * var) - logf(std_[o]) - 0.91893853320467274178f;
+  }
+  // ---- outputs --------------------------------------------------------------
+  const bool keep = alive && live;
+  if (a.full) {
+    f64x4 v = {alive ? (double)act[0] : 0.0, alive ? (double)act[1] : 0.0, alive ? (double)act[2] : 0.0,
+               alive ? (double)act[3] : 0.0};
+    *(f64x4 *)(a.full + (e * a.A + a.own0 + i) * 4) = v;
+  }
+  if (a.act_out)
+    *(f32x4 *)(a.act_out + e * a.act_env_stride + 4 * i) =
+        keep ? f32x4{act[0], act[1], act[2], act[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.logp_out)
+    *(f32x4 *)(a.logp_out + e * a.act_env_stride + 4 * i) =
+        keep ? f32x4{lp[0], lp[1], lp[2], lp[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// ---------------------------------------------------------------------------
+// After lnw_step (lnw_rollout_post): the rollout's bookkeeping of step t and
+// the critic (network.py:154-172, ppo.py:598-605) on the observations the actor
+// saw (the rollout buffer at step t). One workgroup = 64 envs x n waves, wave w
+// = ship w, lane = env:
+//   fc1: wave w sums ship w's D inputs into partial sums of all 32 outputs
+//        (LDS), then every wave adds the n partials and the bias (tanh);
+//   fc2 / fc3: the 64 outputs split over the waves, exchanged through LDS;
+//   fc4: per-wave partial dots, summed by wave 0;
+//   wave 0 then stores the value (0 after the episode ended), the rewards, the
+//   running flag and the env's new live flag (done == 0 ends it, ppo.py:640).
+// ---------------------------------------------------------------------------
+constexpr int CF1 = 32, CF2 = 64, CF3 = 64;
+
+__global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_args a, int off_w1, int off_b1,
+                                                          int off_w2, int off_b2, int off_w3, int off_b3,
+                                                          int off_w4, int off_b4) {
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const int n = a.n, D = a.D;
+  // dynamic LDS: fc1 partials [n][32][65] | fc2 outputs [64][65] | fc4 partial dots [n][64]
+  float *part = actor_lds;
+  float *h2s = part + n * CF1 * (WAVE + 1);
+  float *dsum = h2s + CF2 * (WAVE + 1);
+  const long long e = (long long)blockIdx.x * WAVE + lane;
+  const bool valid = e < a.E;
+  const bool crit = a.critic != nullptr;
+  cfloat *C = (cfloat *)a.critic;
+  if (crit) {
+    float acc[CF1];
+#pragma unroll
+    for (int o = 0; o < CF1; o++) acc[o] = 0.f;
+    if (valid) {
+      const float *x = a.obs + e * a.obs_env_stride + (long long)w * D;
+      const int kb = w * D;
+      for (int k4 = 0; k4 < D; k4 += 4) {
+        const f32x4 xv = *(const f32x4 *)(x + k4);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float xk = xv[q];
+#pragma unroll
+          for (int o = 0; o < CF1; o++) acc[o] = fmaf(C[off_w1 + (kb + k4 + q) * CF1 + o], xk, acc[o]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CF1; o++) part[(w * CF1 + o) * (WAVE + 1) + lane] = acc[o];
+    __syncthreads();
+    float h1[CF1];
+#pragma unroll
+    for (int o = 0; o < CF1; o++) {
+      float s = C[off_b1 + o];
+      for (int v = 0; v < n; v++) s += part[(v * CF1 + o) * (WAVE + 1) + lane];
+      h1[o] = tanhf(s);
+    }
+    // fc2: outputs o = w, w + n, ... (wave-uniform weights)
+    for (int o = w; o < CF2; o += n) {
+      float s = C[off_b2 + o];
+#pragma unroll
+      for (int k = 0; k < CF1; k++) s = fmaf(C[off_w2 + k * CF2 + o], h1[k], s);
+      h2s[o * (WAVE + 1) + lane] = tanhf(s);
+    }
+    __syncthreads();
+    float dot = 0.f;
+    for (int o = w; o < CF3; o += n) {
+      float s = C[off_b3 + o];
+#pragma unroll
+      for (int k = 0; k < CF2; k++) s = fmaf(C[off_w3 + k * CF3 + o], h2s[k * (WAVE + 1) + lane], s);
+      dot = fmaf(C[off_w4 + o], tanhf(s), dot);
+    }
+    dsum[w * WAVE + lane] = dot;
+    __syncthreads();
+  }
+  if (w != 0 || !valid) return;
+  const bool L = !a.live || a.live[e] != 0;
+  const bool masked = a.stop_at_done != 0;
+  if (crit) {
+    float v = C[off_b4];
+    float s = 0.f;
+    for (int q = 0; q < n; q++) s += dsum[q * WAVE + lane];
+    v += s;
+    a.val[e * a.val_env_stride] = (masked && !L) ? 0.0f : v;
+  }
+  if (a.rew && a.rew_out) {
+    for (int q = 0; q < a.n_rew; q++) {
+      const double rv = a.rew_f64 ? ((const double *)a.rew)[e * a.n_rew + q]
+                                  : (double)((const float *)a.rew)[e * a.n_rew + q];
+      a.rew_out[e * a.rew_env_stride + q] = (masked && !L) ? 0.0 : rv;
+    }
+  }
+  if (a.running) a.running[e * a.running_env_stride] = L ? 1 : 0;
+  if (masked && a.live && a.done) a.live[e] = (L && a.done[e] != 0) ? 1 : 0;
 }
 
 }  // namespace
@@ -182,6 +517,77 @@ int lnw_actor_features(const float *params_dev, int32_t obs_dim, const float *ob
   const int n_par = CONV_PARAMS + 2 * (obs_dim - WIN + 12);
   features_kernel<<<dim3((unsigned)blocks), dim3(CH_THREADS), (n_par + 45 * CH_THREADS) * sizeof(float),
                     (hipStream_t)stream>>>(params_dev, obs_dim, obs_dev, B, bn_running, out_dev);
+  return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
+}
+
+// Packed MLP part of lnw_policy_act's parameters, after the conv head block
+// (BatchedActor.packed_policy()), torch's [out][in] layouts: fc1 W [64][K1]
+// (zero-padded to K1 = 32 columns when n_in <= 32, else 64), b [64]; fc2 W
+// [64][64], b [64]; fc3 W [32][64], b [32]; normal head W [4][32]; log-std
+// head W [4][32].
+int lnw_policy_act(const lnw_policy_args *args, void *stream) {
+  if (!args) return LNW_EINVAL;
+  const lnw_policy_args &a = *args;
+  if (!a.obs || !a.params || !a.alive || a.n <= 0 || a.E < 0 || a.A <= 0 || a.own0 < 0 || a.own0 + a.n > a.A)
+    return LNW_EINVAL;
+  if (a.D < WIN || a.D - WIN + 12 > MAX_IN || (a.D & 3)) return LNW_EUNSUPPORTED;
+  if (a.forced && !a.forced_act) return LNW_EINVAL;
+  if (!a.forced && a.T <= 0) return LNW_EINVAL;
+  if (a.script && (!a.full || a.script_own0 < 0 || a.script_own0 + a.script_cnt > a.A)) return LNW_EINVAL;
+  if ((a.kinds_f32_all_alive || a.f32_out) && !a.kinds) return LNW_EINVAL;
+  // 16-B aligned rows for the vector copies and stores
+  if (((uintptr_t)a.obs & 15) || (a.obs_out && (((uintptr_t)a.obs_out & 15) || (a.obs_env_stride & 3))) ||
+      ((a.act_out || a.logp_out) && (a.act_env_stride & 3)) || (a.act_out && ((uintptr_t)a.act_out & 15)) ||
+      (a.logp_out && ((uintptr_t)a.logp_out & 15)) || (a.full && ((uintptr_t)a.full & 31)) ||
+      (a.script && ((uintptr_t)a.script & 31)))
+    return LNW_EINVAL;
+  if (a.E == 0) return 0;
+  PolicyArgs pa;
+  pa.a = a;
+  pa.n_in = a.D - WIN + 12;
+  int o = CONV_PARAMS + 2 * pa.n_in;
+  const int k1 = pa.n_in <= 32 ? 32 : MAX_IN;  // fc1 columns as packed (zero-padded)
+  pa.off_w1 = o; o += k1 * FC1;
+  pa.off_b1 = o; o += FC1;
+  pa.off_w2 = o; o += FC1 * FC2;
+  pa.off_b2 = o; o += FC2;
+  pa.off_w3 = o; o += FC2 * FC3;
+  pa.off_b3 = o; o += FC3;
+  pa.off_wm = o; o += FC3 * NOUT;
+  pa.off_ws = o;
+  const long long rows = a.E * a.n;
+  const unsigned blocks = (unsigned)((rows + CH_THREADS - 1) / CH_THREADS);
+  const size_t lds = (size_t)(CONV_PARAMS + 2 * pa.n_in + FC1 * CH_THREADS) * sizeof(float);
+  if (pa.n_in <= 32)
+    policy_act_kernel<32><<<blocks, CH_THREADS, lds, (hipStream_t)stream>>>(pa);
+  else
+    policy_act_kernel<MAX_IN><<<blocks, CH_THREADS, lds, (hipStream_t)stream>>>(pa);
+  return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
+}
+
+// Packed critic (BatchedCritic.packed()): fc1 W^T [in][32], b [32]; fc2 W^T
+// [32][64], b [64]; fc3 W^T [64][64], b [64]; fc4 w [64], b [1]; in = n * D.
+int lnw_rollout_post(const lnw_rollout_post_args *args, void *stream) {
+  if (!args) return LNW_EINVAL;
+  const lnw_rollout_post_args &a = *args;
+  if (a.n <= 0 || a.n > 16 || a.E < 0) return LNW_EINVAL;
+  if (a.critic && (!a.obs || !a.val || (a.D & 3) || ((uintptr_t)a.obs & 15) || (a.obs_env_stride & 3)))
+    return LNW_EINVAL;
+  if (a.rew_out && (!a.rew || a.n_rew <= 0)) return LNW_EINVAL;
+  if (a.E == 0) return 0;
+  const int in = a.n * a.D;
+  int o = 0;
+  const int w1 = o; o += in * CF1;
+  const int b1 = o; o += CF1;
+  const int w2 = o; o += CF1 * CF2;
+  const int b2 = o; o += CF2;
+  const int w3 = o; o += CF2 * CF3;
+  const int b3 = o; o += CF3;
+  const int w4 = o; o += CF3;
+  const int b4 = o;
+  const unsigned blocks = (unsigned)((a.E + WAVE - 1) / WAVE);
+  const size_t lds = a.critic ? (size_t)(a.n * CF1 * (WAVE + 1) + CF2 * (WAVE + 1) + a.n * WAVE) * sizeof(float) : 0;
+  rollout_post_kernel<<<blocks, WAVE * a.n, lds, (hipStream_t)stream>>>(a, w1, b1, w2, b2, w3, b3, w4, b4);
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 

@@ -23,7 +23,7 @@ constexpr int OPEN_CAP = 16;      // A* open list bound is 15 (floor(L/2)+8 from
 
 // value kinds: NumPy-2 NEP 50 promotion lattice
 enum { K_PYINT = 0, K_PYFLOAT = 1, K_F32 = 2, K_F64 = 3 };
-enum { T_SMALL = 0, T_LARGE = 1, T_LS = 2 };
+enum { T_SMALL = 0, T_LARGE = 1, T_LS = 2, T_MEDIUM = 3 };
 
 constexpr double PY_PI = 3.141592653589793;
 constexpr double RAD2DEG = 180.0 / PY_PI;  // CPython math.degrees constant
@@ -47,6 +47,8 @@ struct KParams {
   double den[2];      // aggressive-reward denominator per mast class (game.py:269)
   double det_q[2];    // detected_prob: [0] target radar==1 (0.345-0.1), [1] otherwise
   int box_lo[2], box_hi[2];
+  int xcd_remap;      // env chunks dealt to workgroups XCD-contiguously (xcd_chunk); LNW_NO_XCD_REMAP turns it off (A/B)
+  int wc[2];          // observation window cells per side: 49 (7x7), or 25 for a side of medium ships (5x5, game.py:595-610)
   int epw;            // environments per workgroup (<= EPW; fewer when E is small, to fill the CUs)
   int store_wt;       // observation stream stored write-through (sc1): no dirty lines left in L2 at the launch end
   int atan_odd;       // the host's bearing table is odd in dy (degrees(atan2(-dy, dx)) == -degrees(atan2(dy, dx))): the group kernel stages its dy >= 0 half
@@ -75,13 +77,13 @@ struct KState {
   const double *atan_deg;  // [LOS_W][LOS_W] degrees(atan2(dy, dx)), host libm (EW bearings)
   const uint8_t *grid;     // [G][G]
   const float *gridf;      // [G][G] grid/255 as float32
-  const float *winf;       // [2][G*G][52] Combatant | LandingShip observation windows
+  const float *winf;       // [3][G*G][52] Combatant 7x7 | LandingShip 5x5 | medium Combatant 5x5 observation windows
   float *dummy;            // [WAVE * 4] sink for masked-out stores (keeps store counts static)
   unsigned long long *prof;  // diagnostics (LNW_PROF): [n_wg][16] phase timestamps, else null
   lnw_analytics ana;         // analytics side channels (null pointers: off)
   unsigned long long *ctr;   // lnw_set_counters work counters (null: off)
   const uint32_t *mask2;   // [G][W16] 2 bits per cell: bit0 > move_thr, bit1 > ew_thr
-  const uint32_t *mvtab;   // [2][G*G][3]
+  const uint32_t *mvtab;   // [3][G*G][3] move tables: Combatant speed 3 | LandingShip | medium Combatant speed 2
   const uint32_t *lostab;  // [G*G][486]
   const double *tape;
   const long long *tape_off;
@@ -364,7 +366,32 @@ struct Rng {
 // --------------------------------------------------------------------------
 // ship attributes (combatant.py:60-88, landingship.py:61-92)
 // --------------------------------------------------------------------------
-__device__ inline int ship_speed(int t) { return t == T_LS ? 2 : 3; }
+__device__ inline int ship_speed(int t) { return (t == T_LS || t == T_MEDIUM) ? 2 : 3; }
+// move-table / A* class (check_path flavour and speed): Combatant speed 3,
+// LandingShip, medium Combatant (speed 2)
+__host__ __device__ inline int mv_cls(int t) { return t == T_LS ? 1 : (t == T_MEDIUM ? 2 : 0); }
+// observation-window record class: Combatant 7x7, LandingShip 5x5 (asymmetric),
+// medium Combatant 5x5 (combatant.py:165-181 with speed 2)
+__device__ inline int win_cls(int t) { return mv_cls(t); }
+__device__ inline int win_len(int t) { return t == T_SMALL || t == T_LARGE ? 49 : 25; }
+// radar / EW range class of a target: small, large-like (large, medium: mast
+// 30, rcs 1), LandingShip (rcs 0.9)
+__device__ inline int rng_cls(int t) { return t == T_SMALL ? 0 : (t == T_LS ? 2 : 1); }
+// Env chunk of workgroup b of nwg. Workgroups are dealt round-robin over the 8
+// XCDs (b, b + 8, ... share one; speed only, never correctness), and each XCD
+// has its own L2: with consecutive chunks on different XCDs, every cache line a
+// chunk shares with its neighbour (byte and word fields of 16- or 32-env
+// chunks, per-env outputs) is fetched into two or more L2s. Dealing each XCD a
+// contiguous run of chunks keeps those lines in one L2. A bijection on
+// [0, nwg) when nwg is a multiple of 8 (else the identity).
+__device__ __forceinline__ int xcd_chunk(const KParams &P, int b, int nwg) {
+  if (!P.xcd_remap || (nwg & 7)) return b;
+  return (b & 7) * (nwg >> 3) + (b >> 3);
+}
+// observation row length of a side: 4 n + window + 3 (game.py:609-610)
+__device__ inline int side_D(const KParams &P, int side) {
+  return 4 * (side ? P.nr : P.nb) + P.wc[side ? 1 : 0] + 3;
+}
 __device__ inline int mast_cls(int t) { return t == T_SMALL ? 0 : 1; }
 __device__ inline double ship_rcs(int t) { return t == T_SMALL ? 0.7 : (t == T_LS ? 0.9 : 1.0); }
 __device__ inline int missiles0(int t) { return t == T_LS ? 0 : (t == T_SMALL ? 4 : 8); }

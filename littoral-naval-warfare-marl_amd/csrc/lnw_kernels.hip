@@ -37,10 +37,16 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 // clean, so the launch does not end by writing back megabytes of dirty
 // observation lines at the kernel boundary (P.store_wt; the host enables it
 // only while every offset fits the 32-bit buffer range). Else a non-temporal
-// store.
+// store. The base is wave-uniform by contract (every caller passes a block or
+// unit base): it is taken from the first active lane, so the resource is built
+// in SGPRs once and the store never becomes a per-lane waterfall loop.
 __device__ __forceinline__ void st_obs4(f32x4 *base, uint32_t i4, f32x4 v, bool wt) {
   if (wt) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    const uint64_t bp = (uint64_t)(uintptr_t)base;
+    const uint64_t ub = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bp) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bp >> 32)) << 32;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)ub, 0, 0x7fffffff, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, v), rs, i4 * 16u, 0, 16 /* sc1 */);
   } else {
     __builtin_nontemporal_store(v, base + i4);
@@ -258,6 +264,9 @@ struct Ctx {
   // group kernel: this lane's index in its env's group and the group's first
   // lane in the wave (fire_dev<true> tests the opponents across the group)
   int gsub = 0, gsh = 0;
+  // group kernel, work counters bound: EW bearings this lane's opponent
+  // columns had evaluated pooled over the group (lnw_set_counters [3])
+  unsigned pooled = 0;
 #ifdef LNW_GROUP_PROF
   unsigned long long gp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // group-kernel section timers
 #endif
@@ -299,7 +308,7 @@ __device__ inline bool check_path_h(const KParams &P, const KState &S, int type,
   if (tx < 0 || tx > 99 || ty < 0 || ty > 99) return false;
   int ox = tx - sx, oy = ty - sy;
   if (P.move_mode == 0 && ox >= -R_MV && ox <= R_MV && oy >= -R_MV && oy <= R_MV) {
-    int cls = type == T_LS ? 1 : 0;
+    int cls = mv_cls(type);
     int bit = (ox + R_MV) * MV_W + (oy + R_MV);
     uint32_t w = S.mvtab[((size_t)cls * P.G * P.G + (size_t)sx * P.G + sy) * MV_WORDS + (bit >> 5)];
     return (w >> (bit & 31)) & 1u;
@@ -755,11 +764,11 @@ __device__ __forceinline__ void get_obs_dev(Ctx &X, int me) {
       const int dx = pos_x(pj) - pos_x(pi), dy = pos_y(pj) - pos_y(pi);
       const int d2 = dx * dx + dy * dy;
       if (d2 >= X.r2max) continue;  // beyond every radar / EW / close range: LOS unused
-      const int tj = COLB(c.type, j);
-      const int rr0 = tj == T_SMALL ? rr_t[0][0] : (tj == T_LARGE ? rr_t[0][1] : rr_t[0][2]);
-      const int rr1 = tj == T_SMALL ? rr_t[1][0] : (tj == T_LARGE ? rr_t[1][1] : rr_t[1][2]);
-      const int re0 = tj == T_SMALL ? re_t[0][0] : (tj == T_LARGE ? re_t[0][1] : re_t[0][2]);
-      const int re1 = tj == T_SMALL ? re_t[1][0] : (tj == T_LARGE ? re_t[1][1] : re_t[1][2]);
+      const int tj = rng_cls(COLB(c.type, j));  // (rr_t / re_t columns: small, large-like, LandingShip)
+      const int rr0 = tj == 0 ? rr_t[0][0] : (tj == 1 ? rr_t[0][1] : rr_t[0][2]);
+      const int rr1 = tj == 0 ? rr_t[1][0] : (tj == 1 ? rr_t[1][1] : rr_t[1][2]);
+      const int re0 = tj == 0 ? re_t[0][0] : (tj == 1 ? re_t[0][1] : re_t[0][2]);
+      const int re1 = tj == 0 ? re_t[1][0] : (tj == 1 ? re_t[1][1] : re_t[1][2]);
       const int rr = mi ? rr1 : rr0, re = mi ? re1 : re0;
       const bool rad_ok = myradar == 1 && d2 < rr * rr, close = d2 < 16;
       const bool ew_cand = d2 < re * re && COLW(c.radar_cur, j) == 1;
@@ -1844,7 +1853,7 @@ __device__ __forceinline__ void build_row(const KParams &P, const KState &S, con
   const int own0 = side ? P.nb : 0;
   const int ns = side ? P.nr : P.nb;
   const int kl = k - own0;
-  const int D = 4 * ns + 52;
+  const int D = side_D(P, side);
   const int G = P.G;
   if (!c.alive0[k * PADB + el] || (only_observed && !c.obsd[k * PADB + el])) {
     for (int d = 0; d < D; d++) row[d] = 0.0f;
@@ -1854,9 +1863,10 @@ __device__ __forceinline__ void build_row(const KParams &P, const KState &S, con
   const uint32_t p = c.pos_cur[k * PAD + el];
   const int px = pos_x(p), py = pos_y(p);
   int idx;
-  if (tk == T_LS) {
-    // asymmetric 5x5 window rows/cols pos-1..pos+3 (landingship.py:178-188)
-    const f32x4 *w = (const f32x4 *)(S.winf + ((size_t)G * G + (size_t)(px * G + py)) * 52);
+  if (tk == T_LS || tk == T_MEDIUM) {
+    // 5x5 windows: LandingShip rows/cols pos-1..pos+3 (landingship.py:178-188),
+    // medium Combatant pos-2..pos+2 (combatant.py:165-181 at speed 2)
+    const f32x4 *w = (const f32x4 *)(S.winf + ((size_t)win_cls(tk) * G * G + (size_t)(px * G + py)) * 52);
     f32x4 v[7];
 #pragma unroll
     for (int q = 0; q < 7; q++) v[q] = w[q];
@@ -1906,13 +1916,13 @@ __device__ __forceinline__ void build_row(const KParams &P, const KState &S, con
 }
 
 // Copy one side's block [ne envs][ns rows][D] (contiguous in the output, a
-// multiple of 4 floats and 16-B aligned since D = 4*ns + 52) with each lane
-// moving 4 consecutive floats: ds_read_b128 from the staged row, dwordx4 store
-// (1 KiB per wave store instruction).
-__device__ inline void copy_side(const float *stage, float *out, int ns, int ne, long long genv0) {
+// multiple of 4 floats and 16-B aligned since D = 4*ns + 52, or 4*ns + 28 for
+// a side of medium ships) with each lane moving 4 consecutive floats:
+// ds_read_b128 from the staged row, dwordx4 store (1 KiB per wave store
+// instruction).
+__device__ inline void copy_side(const float *stage, float *out, int ns, int D, int ne, long long genv0) {
   if (!out) return;
   const int lane = threadIdx.x & (WAVE - 1);
-  const int D = 4 * ns + 52;
   const int S4 = stage_stride(ns) >> 2;
   const int D4 = D >> 2;
   const int n4 = ne * ns * D4;
@@ -1953,8 +1963,8 @@ __device__ __forceinline__ void write_obs(const KParams &P, const KState &S, Col
       build_row(P, S, c, duct_col, g0 + my_e, my_k, row, xg, only_observed);
     wave_lds_sync();
     if (!(P.dbg_skip & 16)) {
-      copy_side(stage_b, obs_b, nb, ne, env0 + g0);
-      copy_side(stage_r, obs_r, nr, ne, env0 + g0);
+      copy_side(stage_b, obs_b, nb, side_D(P, 0), ne, env0 + g0);
+      copy_side(stage_r, obs_r, nr, side_D(P, 1), ne, env0 + g0);
     }
     wave_lds_sync();
   }
@@ -2428,7 +2438,7 @@ __device__ __forceinline__ bool move_batch_t(const KParams &P, const KState &S, 
       if (P.move_mode == 0 && tx <= 99 && ty <= 99 && ox >= -R_MV && ox <= R_MV && oy >= -R_MV &&
           oy <= R_MV) {
         const int bit = (ox + R_MV) * MV_W + (oy + R_MV);
-        mw[k] = (int)(((size_t)(t == T_LS ? 1 : 0) * P.G * P.G + (size_t)sx * P.G + sy) * MV_WORDS +
+        mw[k] = (int)(((size_t)mv_cls(t) * P.G * P.G + (size_t)sx * P.G + sy) * MV_WORDS +
                       (bit >> 5)) * 32 + (bit & 31);
       }
     }
@@ -2719,7 +2729,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = UN > 1 ? (int)((threadIdx.x / WAVE) & 1) : (int)(threadIdx.x / WAVE);
   const int epw = P.epw;
-  const int env0 = (blockIdx.x * UN + unit) * epw;
+  const int env0 = (UN > 1 ? blockIdx.x * UN + unit : xcd_chunk(P, (int)blockIdx.x, (int)gridDim.x)) * epw;
   // LNW_PROF: one record per unit (prof_stamp writes S.prof[blockIdx.x * PROF_SLOTS + slot])
   if (UN > 1 && S.prof) S.prof += (size_t)(blockIdx.x * (UN - 1) + unit) * PROF_SLOTS;
   const int env = env0 + lane;
@@ -2995,7 +3005,7 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
                                                      float *obs_r) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int epw = P.epw;
-  const int env0 = blockIdx.x * epw;
+  const int env0 = xcd_chunk(P, (int)blockIdx.x, (int)gridDim.x) * epw;
   const int env = env0 + lane;
   const long long E = P.E;
   const bool valid = lane < epw && env < E;
@@ -3071,11 +3081,13 @@ __global__ void build_mask_kernel(const uint8_t *grid, int G, int W16, int move_
 }
 
 // move table: check_path(start, start + off) for off in [-4,4]^2, per class
+// (mv_cls: Combatant speed 3, LandingShip, medium Combatant speed 2)
+constexpr int MV_CLASSES = 3;
 __global__ __launch_bounds__(64) void build_move_table_kernel(const uint32_t *mask2, int G, int W16,
                                                               uint32_t *mvtab) {
   __shared__ uint32_t open[OPEN_CAP * WAVE];
   long long i = (long long)blockIdx.x * WAVE + threadIdx.x;
-  long long n = 2LL * G * G * MV_W * MV_W;
+  long long n = (long long)MV_CLASSES * G * G * MV_W * MV_W;
   if (i >= n) return;
   int off = (int)(i % (MV_W * MV_W));
   long long cell = (i / (MV_W * MV_W)) % ((long long)G * G);
@@ -3083,7 +3095,8 @@ __global__ __launch_bounds__(64) void build_move_table_kernel(const uint32_t *ma
   int sx = (int)(cell / G), sy = (int)(cell % G);
   int tx = sx + off / MV_W - R_MV, ty = sy + off % MV_W - R_MV;
   MaskBlocked mb{mask2, W16};
-  bool feas = check_path_dev(mb, mb(sx, sy), G, cls ? T_LS : T_SMALL, sx, sy, tx, ty,
+  const int type = cls == 0 ? T_SMALL : (cls == 1 ? T_LS : T_MEDIUM);  // (mv_cls inverse)
+  bool feas = check_path_dev(mb, mb(sx, sy), G, type, sx, sy, tx, ty,
                              open + threadIdx.x, WAVE);
   if (feas) atomicOr(&mvtab[(cls * (long long)G * G + cell) * MV_WORDS + (off >> 5)], 1u << (off & 31));
 }
@@ -3091,33 +3104,36 @@ __global__ __launch_bounds__(64) void build_move_table_kernel(const uint32_t *ma
 // LOS table: for every origin cell and offset in [-40,40]^2, bit0 radar clear,
 // bit1 EW clear (full march, no early exit). The 2-bit terrain mask is staged
 // into LDS once per workgroup (mwords words, when it fits the launch's LDS),
-// so the 81 rays of every thread march from LDS.
+// and each workgroup then walks many (cell, row) items in a grid-stride loop,
+// so the mask is read once per resident workgroup rather than once per 256
+// items (G = 512: 64 KiB per workgroup).
 __global__ __launch_bounds__(256) void build_los_table_kernel(const uint32_t *mask2, int G, int W16,
                                                               uint32_t *lostab, int mwords) {
   uint32_t *lm = (uint32_t *)lds_dyn;
   for (int w = threadIdx.x; w < mwords; w += blockDim.x) lm[w] = mask2[w];
   __syncthreads();
   const uint32_t *msk = mwords ? lm : mask2;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long n = (long long)G * G * LOS_W;
-  if (i >= n) return;
-  int row = (int)(i % LOS_W);
-  long long cell = i / LOS_W;
-  int x1 = (int)(cell / G), y1 = (int)(cell % G);
-  int x2 = x1 + row - R_LOS;
-  uint32_t words[LOS_ROW_WORDS] = {0, 0, 0, 0, 0, 0};
-  if (x2 >= 0 && x2 < G) {
-    for (int c = 0; c < LOS_W; c++) {
-      int y2 = y1 + c - R_LOS;
-      if (y2 < 0 || y2 >= G) continue;
-      uint32_t b = los_march<false>(msk, W16, x1, y1, x2, y2);
-      int col = c * 2;
-      words[col >> 5] |= b << (col & 31);
+  const long long n = (long long)G * G * LOS_W;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int row = (int)(i % LOS_W);
+    const long long cell = i / LOS_W;
+    const int x1 = (int)(cell / G), y1 = (int)(cell % G);
+    const int x2 = x1 + row - R_LOS;
+    uint32_t words[LOS_ROW_WORDS] = {0, 0, 0, 0, 0, 0};
+    if (x2 >= 0 && x2 < G) {
+      for (int c = 0; c < LOS_W; c++) {
+        const int y2 = y1 + c - R_LOS;
+        if (y2 < 0 || y2 >= G) continue;
+        const uint32_t b = los_march<false>(msk, W16, x1, y1, x2, y2);
+        const int col = c * 2;
+        words[col >> 5] |= b << (col & 31);
+      }
     }
-  }
-  uint32_t *dst = lostab + cell * LOS_CELL_WORDS + row * LOS_ROW_WORDS;
+    uint32_t *dst = lostab + cell * LOS_CELL_WORDS + row * LOS_ROW_WORDS;
 #pragma unroll
-  for (int w = 0; w < LOS_ROW_WORDS; w++) dst[w] = words[w];
+    for (int w = 0; w < LOS_ROW_WORDS; w++) dst[w] = words[w];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3349,6 +3365,9 @@ struct lnw_handle {
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
+  int last_kernel = LNW_KERNEL_NONE;     // lnw_step_kernel: what the last lnw_step launched
+  bool has_medium = false;               // the spawn spec has medium ships (runtime-size kernels only)
+  unsigned long long terrain_hash = 0;   // FNV-1a of the loaded grid (state snapshots name their terrain)
   uint32_t *d_mask2 = nullptr, *d_mvtab = nullptr, *d_lostab = nullptr;
   uint32_t *pos = nullptr;
   int32_t *radar = nullptr, *steps = nullptr, *envi = nullptr;
@@ -3400,8 +3419,8 @@ size_t step_lds_bytes(const lnw_handle *h) {
 // the step launch's LDS: step_lds_bytes plus the whole-side row stages of
 // small quiet workgroups (the same condition step_kernel evaluates)
 size_t step_launch_lds_bytes(const lnw_handle *h, int epw) {
-  const bool tmpl = !h->force_generic && h->params.los_mode == 0 && h->nb == h->nr && h->nb >= 2 &&
-                    h->nb <= 4 && EPW == WAVE;
+  const bool tmpl = !h->force_generic && !h->has_medium && h->params.los_mode == 0 && h->nb == h->nr &&
+                    h->nb >= 2 && h->nb <= 4 && EPW == WAVE;
   const int rows = tmpl && epw * h->nb <= WAVE ? epw * h->nb : 0;
   LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G, rows);
   return (size_t)L.total;
@@ -3687,6 +3706,8 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
+  // LNW_NO_XCD_REMAP: workgroup b steps env chunk b (A/B tests of xcd_chunk)
+  h->kp.xcd_remap = getenv("LNW_NO_XCD_REMAP") == nullptr ? 1 : 0;
   // write-through observation stores (st_obs4) while a side's output fits the
   // 32-bit buffer offsets; LNW_NO_STORE_WT keeps non-temporal stores (A/B)
   {
@@ -3755,6 +3776,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   k.rng_mode = LNW_RNG_PHILOX;
   k.seed = 0;
   k.epw = EPW;  // refined by lnw_load_terrain (choose_epw) once the LDS size is known
+  k.wc[0] = k.wc[1] = 49;  // 7x7 windows until a reset spawns a side of medium ships
   host_constants(k);
   *out = h;
   return 0;
@@ -3787,21 +3809,27 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   }
   rc |= dalloc(h, &h->d_grid, (size_t)G * G);
   rc |= dalloc(h, &h->d_gridf, (size_t)G * G);
-  rc |= dalloc(h, &h->d_winf, (size_t)2 * G * G * 52);
+  rc |= dalloc(h, &h->d_winf, (size_t)3 * G * G * 52);
   rc |= dalloc(h, &h->d_mask2, (size_t)G * h->W16);
-  rc |= dalloc(h, &h->d_mvtab, (size_t)2 * G * G * MV_WORDS);
+  rc |= dalloc(h, &h->d_mvtab, (size_t)MV_CLASSES * G * G * MV_WORDS);
   rc |= dalloc(h, &h->d_lostab, (size_t)G * G * LOS_CELL_WORDS);
   if (rc) return rc;
   HIPCHK(hipMemcpy(h->d_grid, grid_host, (size_t)G * G, hipMemcpyHostToDevice));
+  {
+    unsigned long long fh = 1469598103934665603ull ^ (unsigned long long)G;
+    for (size_t i = 0; i < (size_t)G * G; i++) fh = (fh ^ grid_host[i]) * 1099511628211ull;
+    h->terrain_hash = fh;
+  }
   {  // observation window values grid/255 (combatant.py:177), float64 quotient -> float32
     std::vector<float> gf((size_t)G * G);
     for (size_t i = 0; i < gf.size(); i++) gf[i] = (float)((double)grid_host[i] / 255.0);
     HIPCHK(hipMemcpy(h->d_gridf, gf.data(), gf.size() * sizeof(float), hipMemcpyHostToDevice));
     // per-cell observation windows, one 52-float (13 x float4) record per cell
     // and class: [0] Combatant 7x7 around the ship (49 floats), [1] LandingShip
-    // 5x5 rows/cols pos-1..pos+3 (25 floats); cells outside the hard-coded
+    // 5x5 rows/cols pos-1..pos+3 (25 floats), [2] medium Combatant 5x5 around
+    // the ship (speed 2: combatant.py:165-181); cells outside the hard-coded
     // 0..99 are 0 (combatant.py:176, landingship.py:183)
-    std::vector<float> wf((size_t)2 * G * G * 52, 0.0f);
+    std::vector<float> wf((size_t)3 * G * G * 52, 0.0f);
     auto cellv = [&](int x, int y) {
       return (0 <= x && x < 100 && 0 <= y && y < 100 && x < G && y < G) ? gf[(size_t)x * G + y] : 0.0f;
     };
@@ -3813,6 +3841,9 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
         float *w5 = &wf[((size_t)G * G + (size_t)x * G + y) * 52];
         for (int i = 0; i < 5; i++)
           for (int j = 0; j < 5; j++) w5[i * 5 + j] = cellv(x - 1 + i, y - 1 + j);
+        float *wm = &wf[((size_t)2 * G * G + (size_t)x * G + y) * 52];
+        for (int i = 0; i < 5; i++)
+          for (int j = 0; j < 5; j++) wm[i * 5 + j] = cellv(x - 2 + i, y - 2 + j);
       }
     HIPCHK(hipMemcpy(h->d_winf, wf.data(), wf.size() * sizeof(float), hipMemcpyHostToDevice));
   }
@@ -3822,13 +3853,20 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
   int n = G * h->W16;
   build_mask_kernel<<<(n + 255) / 256, 256>>>(h->d_grid, G, h->W16, k.move_thr, k.ew_thr, h->d_mask2);
   HIPCHK(hipGetLastError());
-  long long nm = 2LL * G * G * MV_W * MV_W;
+  long long nm = (long long)MV_CLASSES * G * G * MV_W * MV_W;
   build_move_table_kernel<<<(unsigned)((nm + WAVE - 1) / WAVE), WAVE>>>(h->d_mask2, G, h->W16, h->d_mvtab);
   HIPCHK(hipGetLastError());
   long long nl = (long long)G * G * LOS_W;
   const int mwords = G * h->W16 * 4 <= 64 * 1024 ? G * h->W16 : 0;  // terrain mask staged in LDS
-  build_los_table_kernel<<<(unsigned)((nl + 255) / 256), 256, (size_t)mwords * 4>>>(h->d_mask2, G, h->W16,
-                                                                                     h->d_lostab, mwords);
+  {  // a few resident rounds of workgroups, each looping over its items
+    int ncu = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess && prop.multiProcessorCount > 0)
+      ncu = prop.multiProcessorCount;
+    const long long need = (nl + 255) / 256, cap = (long long)ncu * 8;
+    build_los_table_kernel<<<(unsigned)(need < cap ? need : cap), 256, (size_t)mwords * 4>>>(
+        h->d_mask2, G, h->W16, h->d_lostab, mwords);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   h->terrain = true;
@@ -3891,16 +3929,31 @@ int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn
   if (!h || !spawn) return fail(LNW_EINVAL, "null argument");
   if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
   HIPCHK(hipSetDevice(h->device));
+  int nmed[2] = {0, 0};
   for (int a = 0; a < h->A; a++) {
     int t = spawn->types[a];
-    if (t != LNW_SMALL && t != LNW_LARGE && t != LNW_LS)
-      return fail(LNW_EUNSUPPORTED, "ship type must be small, large or ls");
+    if (t != LNW_SMALL && t != LNW_LARGE && t != LNW_LS && t != LNW_MEDIUM)
+      return fail(LNW_EUNSUPPORTED, "ship type must be small, large, ls or medium");
+    if (t == LNW_MEDIUM) nmed[a >= h->nb]++;
     if (h->params.discrete && t == LNW_LS)
       return fail(LNW_EUNSUPPORTED, "LandingShip has no value_to_coordinates (DISCRETE mode)");
     if (!spawn->rand_ls[a] && (spawn->pos[a][0] < 0 || spawn->pos[a][0] >= h->G ||
                                spawn->pos[a][1] < 0 || spawn->pos[a][1] >= h->G))
       return fail(LNW_EINVAL, "spawn position outside the grid");
   }
+  // a side's row length follows its fastest ship (game.py:595-610), and a
+  // medium ship's get_obs row has a 5x5 window (combatant.py:165-181): a side
+  // of medium ships only has 4 n + 28-float rows; medium ships beside speed-3
+  // ships make the reference's row assignment raise (game.py:344, 381)
+  for (int sd = 0; sd < 2; sd++) {
+    const int ns = sd ? h->nr : h->nb;
+    if (nmed[sd] && nmed[sd] != ns)
+      return fail(LNW_EUNSUPPORTED, "medium ships need a side of medium ships only (the reference's "
+                                    "rows are sized by the fastest ship, game.py:595-610)");
+  }
+  h->kp.wc[0] = nmed[0] ? 25 : 49;
+  h->kp.wc[1] = nmed[1] ? 25 : 49;
+  h->has_medium = nmed[0] || nmed[1];
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipMemcpy(h->sp_types, spawn->types, sizeof(int32_t) * h->A, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->sp_pos, spawn->pos, sizeof(int32_t) * 2 * h->A, hipMemcpyHostToDevice));
@@ -3939,8 +3992,9 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   size_t lds = step_launch_lds_bytes(h, k.epw);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
+  // (medium ships: 5x5 windows and shorter rows, the runtime-size kernels only)
   bool generic = h->force_generic;
-  const bool templated = k.los_mode != 2 && !generic && h->nb == h->nr && h->nb >= 2 && h->nb <= 4;
+  const bool templated = k.los_mode != 2 && !generic && !h->has_medium && h->nb == h->nr && h->nb >= 2 && h->nb <= 4;
   const bool use_group = k.los_mode != 2 && !templated && !generic && !h->no_group && h->group_fits;
   // 4v4 at 64 envs per workgroup in LOS-table mode, whole units (the headline):
   // the units kernel (LNW_NO_UNITS keeps one unit per workgroup)
@@ -3964,6 +4018,10 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
                                                  obs_red_dev, rew_blue_dev, rew_red_dev,        \
                                                  done_dev, cog_dev)
   const bool cw = h->contact;
+  h->last_kernel = units ? LNW_KERNEL_UNITS
+                   : k.los_mode == 2 ? LNW_KERNEL_REFLOS
+                   : templated ? (cw ? LNW_KERNEL_TEAM_CONTACT : LNW_KERNEL_TEAM)
+                   : use_group ? LNW_KERNEL_GROUP : LNW_KERNEL_GENERIC;
   if (units) {
     // 4 units of 64 envs per workgroup, one workgroup per CU (step_kernel UN)
     step_kernel<4, 4, false, false, UNITS><<<dim3(h->E / (EPW * UNITS)), dim3(2 * WAVE * UNITS),
@@ -3972,9 +4030,9 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
         cog_dev);
   }
   else if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
-  else if (!generic && h->nb == 4 && h->nr == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
-  else if (!generic && h->nb == 3 && h->nr == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
-  else if (!generic && h->nb == 2 && h->nr == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
+  else if (templated && h->nb == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
+  else if (templated && h->nb == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
+  else if (templated && h->nb == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
   else if (use_group) {
     // runtime team sizes: GL lanes per env (lnw_group.inc)
     const GroupLds gl = group_lds(lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G), h->G * h->W16,
@@ -4002,7 +4060,7 @@ int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_re
   size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + h->kp.epw - 1) / h->kp.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
-  const bool tmpl = !h->force_generic && h->params.los_mode != 2 && h->nb == h->nr;
+  const bool tmpl = !h->force_generic && !h->has_medium && h->params.los_mode != 2 && h->nb == h->nr;
   const bool cw = h->contact;
 #define LNW_OBS(NB_, CW_) \
   observe_kernel<NB_, NB_, CW_><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev)
@@ -4039,6 +4097,130 @@ int lnw_state_field(lnw_handle *h, int32_t field, void **dev_ptr, int64_t *nbyte
 }
 
 int lnw_tlist_cap(lnw_handle *h) { return h ? h->T : LNW_EINVAL; }
+
+int lnw_step_kernel(lnw_handle *h) { return h ? h->last_kernel : LNW_EINVAL; }
+
+// ---- whole-state snapshots (lnw_state_bytes / lnw_get_state / lnw_set_state)
+// Snapshot layout: a 128-byte header (below), then the LNW_NFIELDS state
+// fields in field order, then the spawn spec the in-kernel auto-reset reads
+// (types, cells, randint flags: 64 x i32, 64 x 2 x i32, 64 x i32) and the
+// per-env spawn cells ([E][A][2] i32, zeros when the last reset had none);
+// every section starts on a 256-byte boundary.
+namespace {
+struct StateHeader {
+  char magic[8];            // "LNWSTATE"
+  uint32_t version;         // 1
+  int32_t E, nb, nr, T, G;
+  int32_t rng_mode;         // LNW_RNG_*
+  int32_t pos_env_on;       // the auto-reset respawns on per-env cells
+  uint64_t seed;
+  uint64_t terrain_hash;    // FNV-1a of the grid loaded when the snapshot was taken
+  int64_t total;            // snapshot bytes
+  int32_t box_lo[2], box_hi[2];
+  int32_t abi;              // LNW_ABI_VERSION
+  uint8_t pad[128 - 8 - 4 - 7 * 4 - 3 * 8 - 4 * 4 - 4];
+};
+static_assert(sizeof(StateHeader) == 128, "state header is 128 bytes");
+
+struct Section { void *dev; int64_t bytes; };
+
+int state_sections(lnw_handle *h, std::vector<Section> &out) {
+  out.clear();
+  for (int f = 0; f < LNW_NFIELDS; f++) {
+    void *p = nullptr;
+    int64_t n = 0;
+    if (int rc = lnw_state_field(h, f, &p, &n)) return rc;
+    out.push_back({p, n});
+  }
+  out.push_back({h->sp_types, 64 * 4});
+  out.push_back({h->sp_pos, 128 * 4});
+  out.push_back({h->sp_randls, 64 * 4});
+  out.push_back({h->sp_pos_env, (int64_t)h->E * h->A * 2 * 4});  // (may not be allocated yet)
+  return 0;
+}
+
+inline int64_t sec_align(int64_t v) { return (v + 255) & ~(int64_t)255; }
+}  // namespace
+
+int64_t lnw_state_bytes(lnw_handle *h) {
+  if (!h) return fail(LNW_EINVAL, "null handle");
+  std::vector<Section> s;
+  if (int rc = state_sections(h, s)) return rc;
+  int64_t o = 256;
+  for (const Section &x : s) o += sec_align(x.bytes);
+  return o;
+}
+
+int lnw_get_state(lnw_handle *h, void *dst, int64_t nbytes, void *stream) {
+  if (!h || !dst) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  const int64_t total = lnw_state_bytes(h);
+  if (nbytes < total) return fail(LNW_EINVAL, "snapshot buffer smaller than lnw_state_bytes()");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  StateHeader hd;
+  memset(&hd, 0, sizeof hd);
+  memcpy(hd.magic, "LNWSTATE", 8);
+  hd.version = 1;
+  hd.E = h->E; hd.nb = h->nb; hd.nr = h->nr; hd.T = h->T; hd.G = h->G;
+  hd.rng_mode = h->kp.rng_mode;
+  hd.pos_env_on = h->sp_pos_env_on ? 1 : 0;
+  hd.seed = h->kp.seed;
+  hd.terrain_hash = h->terrain_hash;
+  hd.total = total;
+  for (int i = 0; i < 2; i++) { hd.box_lo[i] = h->kp.box_lo[i]; hd.box_hi[i] = h->kp.box_hi[i]; }
+  hd.abi = LNW_ABI_VERSION;
+  std::vector<Section> s;
+  if (int rc = state_sections(h, s)) return rc;
+  char *d = (char *)dst;
+  char hbuf[256] = {0};
+  memcpy(hbuf, &hd, sizeof hd);
+  HIPCHK(hipMemcpy(d, hbuf, sizeof hbuf, hipMemcpyDefault));
+  int64_t o = 256;
+  for (const Section &x : s) {
+    if (x.dev) {
+      HIPCHK(hipMemcpy(d + o, x.dev, (size_t)x.bytes, hipMemcpyDefault));
+    } else {  // per-env spawn cells never given: zeros (host or device destination)
+      const std::vector<char> z((size_t)x.bytes, 0);
+      HIPCHK(hipMemcpy(d + o, z.data(), (size_t)x.bytes, hipMemcpyDefault));
+    }
+    o += sec_align(x.bytes);
+  }
+  return 0;
+}
+
+int lnw_set_state(lnw_handle *h, const void *src, int64_t nbytes, void *stream) {
+  if (!h || !src) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (nbytes < (int64_t)sizeof(StateHeader)) return fail(LNW_EINVAL, "snapshot too short");
+  StateHeader hd;
+  HIPCHK(hipMemcpy(&hd, src, sizeof hd, hipMemcpyDefault));
+  if (memcmp(hd.magic, "LNWSTATE", 8) != 0 || hd.version != 1)
+    return fail(LNW_EINVAL, "not an lnw state snapshot (bad magic or version)");
+  const int64_t total = lnw_state_bytes(h);
+  if (hd.E != h->E || hd.nb != h->nb || hd.nr != h->nr || hd.T != h->T || hd.G != h->G || hd.total != total)
+    return fail(LNW_EINVAL, "snapshot shape (envs, team sizes, grid) differs from this handle");
+  if (hd.terrain_hash != h->terrain_hash) return fail(LNW_EINVAL, "snapshot was taken on another terrain");
+  if (nbytes < total) return fail(LNW_EINVAL, "snapshot shorter than its header says");
+  if (hd.rng_mode == LNW_RNG_TAPE && (!h->tape || !h->tape_off))
+    return fail(LNW_ESTATE, "snapshot is in tape mode: bind the tape (lnw_set_rng) before restoring");
+  if (hd.pos_env_on && !h->sp_pos_env && dalloc(h, &h->sp_pos_env, (size_t)h->E * h->A * 2)) return LNW_ENOMEM;
+  std::vector<Section> s;
+  if (int rc = state_sections(h, s)) return rc;
+  const char *p = (const char *)src;
+  int64_t o = 256;
+  for (const Section &x : s) {
+    if (x.dev) HIPCHK(hipMemcpy(x.dev, p + o, (size_t)x.bytes, hipMemcpyDefault));
+    o += sec_align(x.bytes);
+  }
+  h->kp.rng_mode = hd.rng_mode;
+  if (hd.rng_mode == LNW_RNG_PHILOX) h->kp.seed = hd.seed;
+  for (int i = 0; i < 2; i++) { h->kp.box_lo[i] = hd.box_lo[i]; h->kp.box_hi[i] = hd.box_hi[i]; }
+  h->sp_pos_env_on = hd.pos_env_on != 0;
+  return 0;
+}
 
 int lnw_set_counters(lnw_handle *h, uint64_t *counters_dev) {
   if (!h) return fail(LNW_EINVAL, "null handle");

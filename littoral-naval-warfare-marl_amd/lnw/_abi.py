@@ -10,7 +10,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblnw.so")
 
-LNW_SMALL, LNW_LARGE, LNW_LS = 0, 1, 2
+LNW_SMALL, LNW_LARGE, LNW_LS, LNW_MEDIUM = 0, 1, 2, 3
 LNW_ACT_F32, LNW_ACT_F64, LNW_ACT_I32 = 0, 1, 2
 LNW_KIND_PYFLOAT, LNW_KIND_F32, LNW_KIND_F64 = 1, 2, 3
 LNW_RNG_PHILOX, LNW_RNG_TAPE = 0, 1
@@ -28,7 +28,13 @@ SYMBOLS = [
     "lnw_set_counters",
     "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
     "lnw_fill_uniform_f32", "lnw_hit_tables", "lnw_set_analytics", "lnw_actor_features",
+    "lnw_state_bytes", "lnw_get_state", "lnw_set_state", "lnw_step_kernel",
+    "lnw_policy_act", "lnw_rollout_post",
 ]
+
+# lnw_step_kernel codes (include/lnw.h LNW_KERNEL_*)
+(KERNEL_NONE, KERNEL_GENERIC, KERNEL_TEAM, KERNEL_TEAM_CONTACT, KERNEL_UNITS, KERNEL_GROUP,
+ KERNEL_REFLOS) = range(7)
 
 
 class Analytics(C.Structure):  # include/lnw.h: lnw_analytics
@@ -49,6 +55,31 @@ class Spawn(C.Structure):
     _fields_ = [("types", C.c_int32 * 64), ("pos", (C.c_int32 * 2) * 64),
                 ("rand_ls", C.c_int32 * 64), ("box_lo", C.c_int32 * 2),
                 ("box_hi", C.c_int32 * 2)]
+
+
+class PolicyArgs(C.Structure):  # include/lnw.h: lnw_policy_args
+    _fields_ = [("obs", C.c_void_p), ("E", C.c_int64),
+                ("n", C.c_int32), ("D", C.c_int32), ("own0", C.c_int32), ("A", C.c_int32),
+                ("params", C.c_void_p), ("bn_running", C.c_int32), ("forced", C.c_int32),
+                ("forced_act", C.c_void_p), ("fa_env_stride", C.c_int64), ("noise", C.c_float),
+                ("seed", C.c_uint64), ("call_dev", C.c_void_p),
+                ("T", C.c_int32), ("t", C.c_int32), ("which", C.c_int32),
+                ("row_base", C.c_int64), ("alive", C.c_void_p), ("live", C.c_void_p),
+                ("obs_out", C.c_void_p), ("obs_env_stride", C.c_int64),
+                ("act_out", C.c_void_p), ("logp_out", C.c_void_p), ("act_env_stride", C.c_int64),
+                ("full", C.c_void_p), ("script", C.c_void_p),
+                ("script_n", C.c_int32), ("script_steps", C.c_int32), ("script_own0", C.c_int32),
+                ("script_cnt", C.c_int32), ("kinds", C.c_void_p), ("kinds_f32_all_alive", C.c_int32),
+                ("f32_out", C.c_void_p), ("f32_env_stride", C.c_int64)]
+
+
+class RolloutPostArgs(C.Structure):  # include/lnw.h: lnw_rollout_post_args
+    _fields_ = [("obs", C.c_void_p), ("obs_env_stride", C.c_int64), ("E", C.c_int64),
+                ("n", C.c_int32), ("D", C.c_int32), ("critic", C.c_void_p), ("val", C.c_void_p),
+                ("val_env_stride", C.c_int64), ("rew", C.c_void_p), ("rew_f64", C.c_int32),
+                ("n_rew", C.c_int32), ("rew_out", C.c_void_p), ("rew_env_stride", C.c_int64),
+                ("done", C.c_void_p), ("live", C.c_void_p), ("running", C.c_void_p),
+                ("running_env_stride", C.c_int64), ("stop_at_done", C.c_int32)]
 
 
 class LnwError(RuntimeError):
@@ -95,6 +126,12 @@ def load(path=None):
         "lnw_hit_tables": ([P, P], C.c_int),
         "lnw_set_analytics": ([P, P], C.c_int),
         "lnw_actor_features": ([P, I32, P, I64, I32, P, P], C.c_int),
+        "lnw_state_bytes": ([P], C.c_int64),
+        "lnw_get_state": ([P, P, I64, P], C.c_int),
+        "lnw_set_state": ([P, P, I64, P], C.c_int),
+        "lnw_step_kernel": ([P], C.c_int),
+        "lnw_policy_act": ([C.POINTER(PolicyArgs), P], C.c_int),
+        "lnw_rollout_post": ([C.POINTER(RolloutPostArgs), P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -19,12 +19,21 @@ import torch
 from . import _abi
 from ._abi import (F_ALIVE, F_DIST_LZ, F_DUCT, F_ENV, F_ERR, F_MISSILES, F_MKIND, F_POS,
                    F_RADAR, F_RNG, F_STEPS, F_TL, F_TL_CNT, F_TYPE, LNW_ACT_F32, LNW_ACT_F64,
-                   LNW_ACT_I32, LNW_LARGE, LNW_LS, LNW_RNG_PHILOX, LNW_RNG_TAPE, LNW_SMALL, Spawn,
+                   LNW_ACT_I32, LNW_LARGE, LNW_LS, LNW_MEDIUM, LNW_RNG_PHILOX, LNW_RNG_TAPE, LNW_SMALL,
+                   Spawn,
                    check)
 from .config import Scenario
 
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
-TYPE_CODES = {"small": LNW_SMALL, "large": LNW_LARGE, "ls": LNW_LS}
+TYPE_CODES = {"small": LNW_SMALL, "large": LNW_LARGE, "ls": LNW_LS, "medium": LNW_MEDIUM}
+
+
+def side_obs_dim(types):
+    """Observation row length of a side (game.py:595-610): 4 per ship plus the
+    movement window of its fastest ship, (2 * speed + 1)^2 cells, plus 3. Only
+    a side of medium ships (speed 2) has 5x5 windows."""
+    codes = [TYPE_CODES.get(t, t) for t in types]
+    return 4 * len(codes) + (25 if codes and all(c == LNW_MEDIUM for c in codes) else 49) + 3
 
 # field -> (torch dtype of the raw bytes, shape builder)
 _FIELDS = {
@@ -67,7 +76,7 @@ class BatchedGame:
         self.red_types = [TYPE_CODES.get(t, t) for t in red_types]
         self.nb, self.nr = len(self.blue_types), len(self.red_types)
         self.A = self.nb + self.nr
-        self.Db, self.Dr = 4 * self.nb + 52, 4 * self.nr + 52
+        self.Db, self.Dr = side_obs_dim(self.blue_types), side_obs_dim(self.red_types)
         self.device = torch.device("cuda", device)
         self.env_id_base = int(env_id_base)
         self._params = self.sc.params()
@@ -320,6 +329,31 @@ class BatchedGame:
         cnt = self.get(F_TL_CNT).cpu().numpy().astype(np.int64)[:, env]
         tl = self.get(F_TL).cpu().numpy().astype(np.int64)[:, :, env] & 0xffff
         return [[(int(v & 0xff), int(v >> 8)) for v in tl[a, :cnt[a]]] for a in range(self.A)]
+
+    def step_kernel(self):
+        """Which step kernel the last step() launched (lnw_step_kernel:
+        _abi.KERNEL_*): build-side launch shape, for tests and diagnostics."""
+        return self.L.lnw_step_kernel(self.h)
+
+    def get_state(self, device="cpu"):
+        """Whole-state snapshot (lnw_get_state) as a uint8 tensor on `device`:
+        every state field, the auto-reset's spawn spec and the RNG mode/seed.
+        Waits for the current stream."""
+        n = self.L.lnw_state_bytes(self.h)
+        if n < 0:
+            check(n)
+        dev = torch.device(device)
+        buf = torch.zeros(n, dtype=torch.uint8, device=dev, pin_memory=False)
+        check(self.L.lnw_get_state(self.h, _ptr(buf), n, self._stream()))
+        return buf
+
+    def set_state(self, snapshot):
+        """Restore a get_state() snapshot (lnw_set_state) taken from a handle of
+        the same shape and terrain; stepping then continues exactly as the
+        saved handle would have. A tape-mode snapshot needs the same tape bound
+        (set_tape) first."""
+        buf = torch.as_tensor(snapshot, dtype=torch.uint8).contiguous()
+        check(self.L.lnw_set_state(self.h, _ptr(buf), buf.numel(), self._stream()))
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

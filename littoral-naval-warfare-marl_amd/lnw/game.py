@@ -32,8 +32,8 @@ from . import _abi
 from .batched import BatchedGame, default_grid
 from .config import Scenario
 
-_TYPES = {"small": 0, "large": 1, "ls": 2}
-_NAMES = {0: "small", 1: "large", 2: "ls"}
+_TYPES = {"small": 0, "large": 1, "ls": 2, "medium": 3}
+_NAMES = {0: "small", 1: "large", 2: "ls", 3: "medium"}
 _DEFAULT_BLUE = {2: [(6, 61), (10, 81)], 3: [(6, 61), (10, 81), (8, 70)],
                  4: [(6, 61), (10, 81), (8, 70), (11, 58)]}   # game.py:551-556
 _LZ = (14, 82)                                                  # game.py:590
@@ -78,7 +78,7 @@ class ShipProxy:
         self._i = index
         self.side = side
         self.ship_type = ship_type
-        self.speed = 2 if ship_type == "ls" else 3
+        self.speed = 2 if ship_type in ("ls", "medium") else 3   # combatant.py:64
         self.line_of_sight = 4
         self.radar_coverage = 20
         self.missile_range = 60
@@ -251,8 +251,10 @@ class Game:
         ms_r = max(s.speed for s in self.red_ships)
         self.blue_movement = ms_b * 2 + 1
         self.red_movement = ms_r * 2 + 1
-        self.observation_space = len(self.blue_ships) * 4 + 49 + 3   # game.py:609 (D = 4n+52)
-        self.red_observation_space = len(self.red_ships) * 4 + 49 + 3
+        # game.py:609-610: 4 n + (2 * fastest speed + 1)^2 + 3 (the 7x7 window
+        # unless the side is all medium ships: the rows the kernel writes)
+        self.observation_space = self._g.Db
+        self.red_observation_space = self._g.Dr
         for s in self._all:
             s.n_obs = self.observation_space
         self.n_blue_left = len(self.blue_ships)

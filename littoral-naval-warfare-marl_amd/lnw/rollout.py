@@ -78,6 +78,19 @@ class BatchedActor(nn.Module):
                  self.layernorm.weight, self.layernorm.bias]
         return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
 
+    def packed_policy(self):
+        """Every parameter lnw_policy_act reads (csrc/lnw_actor.hip), in its order:
+        packed_features(), then the MLP in torch's [out][in] layouts: fc1 W
+        zero-padded to 32 columns (64 when n_in > 32), fc1 b, fc2 W, b, fc3 W, b,
+        normal_head W, log_std_head W."""
+        n_in = self.layernorm.normalized_shape[0]
+        k1 = 32 if n_in <= 32 else 64
+        w1 = torch.zeros((64, k1), dtype=torch.float32, device=self.fc1.weight.device)
+        w1[:, :n_in] = self.fc1.weight.detach().float()
+        parts = [self.packed_features(), w1, self.fc1.bias, self.fc2.weight, self.fc2.bias,
+                 self.fc3.weight, self.fc3.bias, self.normal_head.weight, self.log_std_head.weight]
+        return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
+
     def features(self, obs, bn="sample"):
         """network.py:70-85 up to the LayerNorm -> [B, n_in]: the HIP kernel
         for device tensors (lnw_actor_features), torch ops for host tensors."""
@@ -159,6 +172,13 @@ class BatchedCritic(nn.Module):
     def load_reference(self, state_dict):
         self.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()})
         return self
+
+    def packed(self):
+        """Parameters in lnw_rollout_post's order (csrc/lnw_actor.hip): fc1 W^T
+        [in][32], b; fc2 W^T [32][64], b; fc3 W^T [64][64], b; fc4 w [64], b."""
+        parts = [self.fc1.weight.t(), self.fc1.bias, self.fc2.weight.t(), self.fc2.bias,
+                 self.fc3.weight.t(), self.fc3.bias, self.fc4.weight, self.fc4.bias]
+        return torch.cat([p.detach().contiguous().reshape(-1).float() for p in parts]).contiguous()
 
     def forward(self, x):
         x = torch.flatten(x, 1)
@@ -269,6 +289,15 @@ class Rollout:
          buffer with per-row value kinds (include/lnw.h);
       4. the critic scores the concatenated blue observations (ppo.py:598-605).
 
+    impl="hip" (default) runs a step as four launches: lnw_observe, the fused
+    policy kernel (lnw_policy_act: conv head, MLP, heads, keyed sample, log-
+    probability, the action array with scripted red rows and row kinds, and
+    the rollout rows; a second launch for a red actor), lnw_step, and
+    lnw_rollout_post (critic, rewards, running / live flags). impl="torch" is
+    the same rollout as batched torch ops (the features kernel + hipBLASLt
+    GEMMs + ~45 small kernels per step), kept as the reference implementation
+    the fused path is tested against.
+
     Rewards are kept in float64 (the reference's floats). With `stop_at_done`
     an env's steps after its first done == 0 are masked out (observations,
     actions, log-probabilities, values and rewards zero, `running` False), as
@@ -283,11 +312,14 @@ class Rollout:
       * sunk ships' action rows are stored as zeros (the reference stores the
         previous ship's `action` variable there, ppo.py:516-517).
 
-    `keyed_seed`: sampling draws come from keyed_normal (Philox keyed by the
-    global env id, the rollout index and the step) instead of a torch
-    generator, so a rollout sharded over ranks by env_id_base samples exactly
-    what one rank over all envs samples (eager runs; a captured graph freezes
-    the keys of the capture).
+    Sampling: keyed draws (keyed_normal: Philox keyed by the seed, the global
+    row, the rollout index and the step), so a rollout sharded over ranks by
+    env_id_base samples exactly what one rank over all envs samples. The
+    rollout index lives in a device counter (`call_index`) that every rollout
+    advances — inside a captured graph too, so each replay draws fresh values.
+    The hip impl always samples this way (seed `keyed_seed`, else `seed`); the
+    torch impl does when `keyed_seed` is given, else it draws from the torch
+    `generator` passed to run().
 
     `observe="step"` reuses the step's own output rows instead of a fresh
     observe (one launch less per step, but not the reference's draw order).
@@ -298,15 +330,26 @@ class Rollout:
 
     def __init__(self, game: BatchedGame, actor, critic=None, steps=40, red="script",
                  red_actor=None, noise=None, bn="sample", red_bn="running", gamma=0.99,
-                 stop_at_done=True, observe="fresh", keyed_seed=None):
+                 stop_at_done=True, observe="fresh", keyed_seed=None, impl="hip", seed=0):
         if observe not in ("fresh", "step"):
             raise ValueError("observe must be 'fresh' or 'step'")
-        self.keyed_seed, self._calls = keyed_seed, 0
+        if impl not in ("hip", "torch"):
+            raise ValueError("impl must be 'hip' or 'torch'")
+        self.keyed_seed, self.impl, self.seed = keyed_seed, impl, int(seed)
         self.g, self.actor, self.critic = game, actor, critic
         self.T, self.red, self.red_actor = int(steps), red, red_actor
         self.noise, self.bn, self.red_bn = noise, bn, red_bn
         self.gamma, self.stop_at_done, self.observe = float(gamma), stop_at_done, observe
         self.table = red_script_table(game.device) if red == "script" else None
+        # rollout index of the keyed draws, on the device (advanced by run())
+        self._call = torch.zeros(1, dtype=torch.int64, device=game.device)
+
+    def call_index(self, value=None):
+        """The device rollout counter the keyed draws are keyed by (read, or set
+        to `value`)."""
+        if value is not None:
+            self._call.fill_(int(value))
+        return int(self._call.item())
 
     @torch.no_grad()
     def run(self, generator=None, forced_actions=None, on_step=None):
@@ -314,32 +357,124 @@ class Rollout:
         is called after step t's launch with the step outputs (device tensors),
         where ppo.py:620-638 does its per-step bookkeeping and logging; it must
         not be given while capturing a graph if it synchronises."""
+        if self.impl == "hip":
+            return self._run_hip(forced_actions, on_step)
+        return self._run_torch(generator, forced_actions, on_step)
+
+    def _buffers(self):
+        g = self.g
+        E, nb, A, D, T, dev = g.E, g.nb, g.A, g.Db, self.T, g.device
+        return dict(obs=torch.zeros((E, T, nb, D), dtype=torch.float32, device=dev),
+                    actions=torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev),
+                    log_probs=torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev),
+                    rewards=torch.zeros((E, T, nb), dtype=torch.float64, device=dev),
+                    values=torch.zeros((E, T), dtype=torch.float32, device=dev),
+                    running=torch.ones((E, T), dtype=torch.bool, device=dev),
+                    f32_step=torch.zeros((E, T), dtype=torch.bool, device=dev))
+
+    def _run_hip(self, forced_actions, on_step):
+        import ctypes as C
+        from . import _abi
+        from ._abi import F_ALIVE, PolicyArgs, RolloutPostArgs
+        L = _abi.load()
+        g = self.g
+        E, nb, nr, A, Db, Dr, T = g.E, g.nb, g.nr, g.A, g.Db, g.Dr, self.T
+        dev = g.device
+        b = self._buffers()
+        obs, acts, logp, rew, val, running, f32s = (b[k] for k in ("obs", "actions", "log_probs", "rewards",
+                                                                "values", "running", "f32_step"))
+        full = torch.zeros((E, A, 4), dtype=torch.float64, device=dev)
+        kinds = torch.full((E, A), _abi.LNW_KIND_F64, dtype=torch.uint8, device=dev)
+        live = torch.ones(E, dtype=torch.bool, device=dev)
+        red_actor_rows = self.red != "script" and self.red_actor is not None
+        ap = self.actor.packed_policy()
+        cp = self.critic.packed() if self.critic is not None else None
+        rap = self.red_actor.packed_policy() if red_actor_rows else None
+        fa = None
+        if forced_actions is not None:
+            fa = forced_actions.to(device=dev, dtype=torch.float32).contiguous()
+            assert fa.shape == (E, T, A, 4)
+        alive_p, _ = g._field(F_ALIVE)
+        seed = int(self.keyed_seed if self.keyed_seed is not None else self.seed) & (2**64 - 1)
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        P = lambda t_: t_.data_ptr()  # noqa: E731
+        f4, f8 = 4, 8
+        table = self.table.contiguous() if self.table is not None else None
+        rew_f64 = int(g.rew_blue.dtype == torch.float64)
+        if self.observe == "step":
+            g.observe(-1)
+        for t in range(T):
+            if self.observe == "fresh":
+                g.observe(-1)
+            pa = PolicyArgs()
+            pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = P(g.obs_blue), E, nb, Db, 0, A
+            pa.params, pa.bn_running = P(ap), int(self.bn == "running")
+            if fa is not None:
+                pa.forced, pa.forced_act, pa.fa_env_stride = 1, P(fa) + t * A * 4 * f4, T * A * 4
+            pa.noise = float(self.noise) if self.noise is not None else 0.0
+            pa.seed, pa.call_dev, pa.T, pa.t, pa.which = seed, P(self._call), T, t, 0
+            pa.row_base = g.env_id_base * nb
+            pa.alive = alive_p
+            pa.live = P(live) if self.stop_at_done else None
+            pa.obs_out, pa.obs_env_stride = P(obs) + t * nb * Db * f4, T * nb * Db
+            pa.act_out, pa.logp_out = P(acts) + t * nb * 4 * f4, P(logp) + t * nb * 4 * f4
+            pa.act_env_stride = T * nb * 4
+            pa.full = P(full)
+            if table is not None:
+                pa.script, pa.script_n, pa.script_steps = P(table), table.shape[0], table.shape[1]
+                pa.script_own0, pa.script_cnt = nb, nr
+            pa.kinds, pa.kinds_f32_all_alive = P(kinds), int(red_actor_rows)
+            pa.f32_out, pa.f32_env_stride = P(f32s) + t, T
+            _abi.check(L.lnw_policy_act(C.byref(pa), stream))
+            if red_actor_rows:
+                ra = PolicyArgs()
+                ra.obs, ra.E, ra.n, ra.D, ra.own0, ra.A = P(g.obs_red), E, nr, Dr, nb, A
+                ra.params, ra.bn_running = P(rap), int(self.red_bn == "running")
+                if fa is not None:
+                    ra.forced, ra.forced_act, ra.fa_env_stride = 1, P(fa) + (t * A + nb) * 4 * f4, T * A * 4
+                ra.seed, ra.call_dev, ra.T, ra.t, ra.which = seed, P(self._call), T, t, 2
+                ra.row_base, ra.alive, ra.full = g.env_id_base * nr, alive_p, P(full)
+                _abi.check(L.lnw_policy_act(C.byref(ra), stream))
+            out = g.step(full, kinds)
+            pp = RolloutPostArgs()
+            pp.obs, pp.obs_env_stride, pp.E, pp.n, pp.D = pa.obs_out, T * nb * Db, E, nb, Db
+            if cp is not None:
+                pp.critic, pp.val, pp.val_env_stride = P(cp), P(val) + t * f4, T
+            pp.rew, pp.rew_f64, pp.n_rew = P(out["rew_blue"]), rew_f64, nb
+            pp.rew_out, pp.rew_env_stride = P(rew) + t * nb * f8, T * nb
+            pp.done, pp.live = P(out["done"]), P(live)
+            pp.running, pp.running_env_stride = P(running) + t, T
+            pp.stop_at_done = int(bool(self.stop_at_done))
+            _abi.check(L.lnw_rollout_post(C.byref(pp), stream))
+            if on_step is not None:
+                on_step(t, out)
+        self._call += 1
+        rtg = reference_rtg(rew, self.gamma)
+        b["rtg"] = rtg
+        return b
+
+    def _run_torch(self, generator, forced_actions, on_step):
         from ._abi import F_ALIVE, LNW_KIND_F32, LNW_KIND_F64
         g = self.g
         E, nb, nr, A, D = g.E, g.nb, g.nr, g.A, g.Db
         dev = g.device
         T = self.T
-        obs = torch.zeros((E, T, nb, D), dtype=torch.float32, device=dev)
-        acts = torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev)
-        logp = torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev)
-        rew = torch.zeros((E, T, nb), dtype=torch.float64, device=dev)
-        val = torch.zeros((E, T), dtype=torch.float32, device=dev)
-        running = torch.ones((E, T), dtype=torch.bool, device=dev)
-        f32_step = torch.zeros((E, T), dtype=torch.bool, device=dev)
+        b = self._buffers()
+        obs, acts, logp, rew, val, running, f32_step = (b[k] for k in (
+            "obs", "actions", "log_probs", "rewards", "values", "running", "f32_step"))
         full = torch.zeros((E, A, 4), dtype=torch.float64, device=dev)
         red_actor_rows = self.red != "script" and self.red_actor is not None
         if self.observe == "step":
             g.observe(-1)
         live = torch.ones(E, dtype=torch.bool, device=dev)
-        call = self._calls
-        self._calls += 1
         base = g.env_id_base
+        call = self._call  # device counter; keyed draws read it on the host here
 
         def draws(t, which, n_side):
             """keyed draws for this step: which 0/1 blue sample / noise, 2 red"""
             if self.keyed_seed is None:
                 return None
-            slot = ((call * T + t) * 4 + which)
+            slot = ((int(call.item()) * T + t) * 4 + which)
             return keyed_normal(base * n_side, E * n_side, 4, self.keyed_seed, slot, dev)
 
         for t in range(T):
@@ -394,20 +529,28 @@ class Rollout:
                 live = live & (out["done"] != 0)
             if on_step is not None:
                 on_step(t, out)
-        rtg = reference_rtg(rew, self.gamma)
+        self._call += 1
         # the learner's advantage is gae(rtg, values) on a sampled minibatch
         # (ppo.py:336), left to the caller as in the reference
-        return dict(obs=obs, actions=acts, log_probs=logp, rewards=rew, values=val,
-                    running=running, f32_step=f32_step, rtg=rtg)
+        b["rtg"] = reference_rtg(rew, self.gamma)
+        return b
 
     def capture(self, generator=None):
-        """Record one whole rollout (T steps of actor, red, critic, step kernel and
-        buffer writes, then reward-to-go and GAE) as a HIP graph, so `replay()`
-        launches its ~30 kernels per step without host work in between. One eager
-        rollout runs first on a side stream (lazy initialisation, GEMM heuristics)
-        and advances the envs; reset before replaying. The graph freezes the
-        step launch's parameters (scenario, spawn spec) and the buffers it
-        returns: `replay()` overwrites them in place."""
+        """Record one whole rollout (T steps of actor, red, critic, step kernel,
+        buffer writes and reward-to-go) as a HIP graph, so `replay()` launches
+        its kernels without host work in between. One eager rollout runs first
+        on a side stream (lazy initialisation, GEMM heuristics) and advances the
+        envs; reset before replaying. The graph freezes the step launch's
+        parameters (scenario, spawn spec) and the buffers it returns: `replay()`
+        overwrites them in place. The rollout counter the keyed draws read is a
+        device tensor the graph advances, so every replay draws fresh values;
+        the torch impl with a `generator` registers it with the graph instead
+        (torch's graph-safe generator offsets). The torch impl with
+        `keyed_seed` cannot be captured (its keyed draws take the counter on the
+        host) and refuses."""
+        if self.impl == "torch" and self.keyed_seed is not None:
+            raise RuntimeError("Rollout(impl='torch', keyed_seed=...) cannot be captured: its keyed "
+                               "draws would be frozen at the capture's rollout index; use impl='hip'")
         dev = self.g.device
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -415,7 +558,7 @@ class Rollout:
             self.run(generator)
         torch.cuda.current_stream(dev).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        if generator is not None:
+        if generator is not None and self.impl == "torch":
             graph.register_generator_state(generator)
         with torch.cuda.graph(graph):
             out = self.run(generator)

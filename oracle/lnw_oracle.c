@@ -1152,7 +1152,7 @@ void orc_fullsize_range(const orc_params *P, const uint8_t *grid, int G, int nb,
                         const int *types, const int *pos, int pos_per_env, const int *rand_ls,
                         uint64_t seed, int64_t E, int64_t env0, int64_t n, int S, int horizon,
                         const float *acts, const uint64_t *mult, uint64_t *hash, float *rew,
-                        int32_t *done_out, float *cog_out) {
+                        int32_t *done_out, float *cog_out, float *acts_after) {
     int A = nb + nr, Db = 4 * nb + 52, Dr = 4 * nr + 52;
     orc_env *e = (orc_env *)malloc(sizeof(orc_env));
     double *act = (double *)malloc(sizeof(double) * 4 * A);
@@ -1186,6 +1186,8 @@ void orc_fullsize_range(const orc_params *P, const uint8_t *grid, int G, int nb,
             }
             int64_t se = (int64_t)s * E + env;
             hash[se] = h;
+            if (acts_after)  /* the action rows as the step left them (game.py:379 write-back) */
+                for (int q = 0; q < 4 * A; q++) acts_after[se * A * 4 + q] = (float)act[q];
             for (int a = 0; a < nb; a++) rew[se * A + a] = (float)rb[a];
             for (int a = 0; a < nr; a++) rew[se * A + nb + a] = (float)rr[a];
             done_out[se] = done;

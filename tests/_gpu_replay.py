@@ -31,7 +31,7 @@ def replay_gpu(fx, grids, los_mode=0, move_mode=0, contact=False):
     types = eps[0]["types"]
     sc = scenario_from_meta(meta, los_mode=los_mode, move_mode=move_mode)
     grid = grids[meta["grid_id"]]
-    names = {0: "small", 1: "large", 2: "ls"}
+    names = {0: "small", 1: "large", 2: "ls", 3: "medium"}
     # float64 rewards / cog: the reference's Python floats, compared with rtol=0
     g = BatchedGame(E, [names[t] for t in types[:nb]], [names[t] for t in types[nb:]],
                     scenario=sc, grid=grid, reward_dtype=torch.float64)

@@ -71,7 +71,7 @@ def lib():
         L.orc_philox.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, P]
         L.orc_fullsize_range.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P,
                                          C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int,
-                                         C.c_int, P, P, P, P, P, P]
+                                         C.c_int, P, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -161,6 +161,10 @@ class OracleEnv:
 
     def reset(self, types, pos, rand_ls=None):
         t = np.ascontiguousarray(types, np.int32)
+        # a side's row length follows its fastest ship (game.py:595-610): a side
+        # of medium ships (speed 2) has 5x5 windows, rows of 4n + 28 floats
+        self.Db_out = 4 * self.nb + (28 if (t[:self.nb] == T_MEDIUM).all() else 52)
+        self.Dr_out = 4 * self.nr + (28 if (t[self.nb:] == T_MEDIUM).all() else 52)
         p = np.ascontiguousarray(pos, np.int32).reshape(-1)
         r = np.ascontiguousarray(rand_ls if rand_ls is not None else np.zeros(self.A), np.int32)
         lib().orc_reset(self.e, _p(t), _p(p), _p(r))
@@ -178,13 +182,17 @@ class OracleEnv:
         cog = np.zeros(1)
         done = lib().orc_step(self.e, _p(act), None if k is None else _p(k), _p(ob), _p(orr),
                               _p(rb), _p(rr), _p(cog))
-        return dict(obs_blue=ob, obs_red=orr, rew_blue=rb, rew_red=rr, done=done, cog=cog[0],
-                    actions_after=act)
+        Db, Dr = getattr(self, "Db_out", self.Db), getattr(self, "Dr_out", self.Dr)
+        assert not ob[:, Db:].any() and not orr[:, Dr:].any()
+        return dict(obs_blue=ob[:, :Db], obs_red=orr[:, :Dr], rew_blue=rb, rew_red=rr, done=done,
+                    cog=cog[0], actions_after=act)
 
     def observe(self, a):
         out = np.zeros(self.Db if a < self.nb else self.Dr)
         lib().orc_observe(self.e, a, _p(out))
-        return out
+        D = getattr(self, "Db_out", self.Db) if a < self.nb else getattr(self, "Dr_out", self.Dr)
+        assert not out[D:].any()
+        return out[:D]
 
     def agents(self):
         A = self.A
@@ -224,11 +232,12 @@ class OracleEnv:
 # golden fixtures
 # ---------------------------------------------------------------------------
 def fullsize(grid, nb, nr, types, pos, acts, mult, seed, horizon, *, pos_per_env=False,
-             rand_ls=None, landing_ops=False, threads=None):
+             rand_ls=None, landing_ops=False, trained_red=True, acts_after=False, threads=None):
     """orc_fullsize_range over all E envs of acts [S, E, A, 4] (float32) on a
     thread pool (ctypes releases the GIL; ranges are disjoint): per (step, env)
     the observation hash (sum bits * mult mod 2^64), float32 rewards [S, E, A],
-    done [S, E] and cog [S, E]."""
+    done [S, E] and cog [S, E]; with acts_after=True also the action rows as
+    each step left them [S, E, A, 4] (an untrained red's salvo write-back)."""
     from concurrent.futures import ThreadPoolExecutor
     L = lib()
     S, E, A = acts.shape[:3]
@@ -238,11 +247,12 @@ def fullsize(grid, nb, nr, types, pos, acts, mult, seed, horizon, *, pos_per_env
     pos = np.ascontiguousarray(pos, np.int32)
     mult = np.ascontiguousarray(mult, np.uint64)
     rls = np.ascontiguousarray(rand_ls if rand_ls is not None else np.zeros(A), np.int32)
-    P = OrcParams(0, int(landing_ops), 1, 1, 1, 0.4, 74, 70, 14, 82)
+    P = OrcParams(0, int(landing_ops), 1, 1, int(trained_red), 0.4, 74, 70, 14, 82)
     hsh = np.zeros((S, E), np.uint64)
     rew = np.zeros((S, E, A), np.float32)
     done = np.zeros((S, E), np.int32)
     cog = np.zeros((S, E), np.float32)
+    aft = np.zeros((S, E, A, 4), np.float32) if acts_after else None
     threads = threads or min(16, os.cpu_count() or 1)
     chunk = (E + threads - 1) // threads
 
@@ -252,9 +262,12 @@ def fullsize(grid, nb, nr, types, pos, acts, mult, seed, horizon, *, pos_per_env
         if n:
             L.orc_fullsize_range(C.byref(P), _p(grid), grid.shape[0], nb, nr, _p(types), _p(pos),
                                  int(pos_per_env), _p(rls), seed, E, e0, n, S, horizon,
-                                 _p(acts), _p(mult), _p(hsh), _p(rew), _p(done), _p(cog))
+                                 _p(acts), _p(mult), _p(hsh), _p(rew), _p(done), _p(cog),
+                                 _p(aft) if aft is not None else None)
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(run, range(threads)))
+    if acts_after:
+        return hsh, rew, done, cog, aft
     return hsh, rew, done, cog
 
 

@@ -641,6 +641,20 @@ def make_episodes(game, combatant, landingship, grids, quick):
     run_scenario(game, combatant, landingship, "8v8_g200_observe", grids,
                  nb_types=["small"] * 8, nr_types=["large"] * 6 + ["ls"] * 2, spawn="melee",
                  n_ep=q(3), seed=15, grid_id=1, observe=True)
+    # the "medium" Combatant (combatant.py:64-80: speed 2, 8 missiles, mast 30,
+    # rcs 1; game.py:193-198). A side's row length follows its fastest ship
+    # (game.py:595-610), and a medium row is 4n + 5x5 + 3 floats, so only a side
+    # made of medium ships runs (mixed with speed-3 ships the row assignment at
+    # game.py:344 raises ValueError)
+    M = ["medium"] * 4
+    run_scenario(game, combatant, landingship, "3v3_medium_melee_observe", grids,
+                 nb_types=M[:3], nr_types=M[:3], spawn="melee", n_ep=q(8), seed=19, observe=True)
+    run_scenario(game, combatant, landingship, "4v2_medium_split_f32", grids, nb_types=M,
+                 nr_types=["large", "small"], spawn="split", n_ep=q(6), seed=20, dtype="f32")
+    run_scenario(game, combatant, landingship, "2v4_medium_discrete", grids, nb_types=S4[:2],
+                 nr_types=M, spawn="melee", n_ep=q(6), seed=24, flags=dict(DISCRETE=True))
+    run_scenario(game, combatant, landingship, "3v3_medium_untrained_red", grids, nb_types=M[:3],
+                 nr_types=M[:3], spawn="melee", n_ep=q(6), seed=25, flags=dict(TRAINED_RED=False))
 
 
 def main():

@@ -22,7 +22,7 @@ def L():
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "lnw.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char \*)\s*(lnw_\w+)\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char \*)\s*(lnw_\w+)\(", src, re.M)))
 
 
 def test_header_symbols_match_binding():
@@ -32,7 +32,7 @@ def test_header_symbols_match_binding():
 def test_library_exports_every_header_symbol(L):
     for s in header_symbols():
         assert hasattr(L, s), s
-    assert L.lnw_abi_version() == 3
+    assert L.lnw_abi_version() == 4
 
 
 def test_hit_tables_match_numpy(L):

@@ -91,3 +91,42 @@ def test_group_kernel_equals_lane_kernel(name, monkeypatch):
         assert torch.equal(an[0][key], an[1][key]), key
     for gm in games:
         gm.close()
+
+
+def test_group_kernel_counts_pooled_bearings(monkeypatch):
+    """lnw_set_counters with the group kernel: counter [3] counts the EW
+    bearings evaluated pooled over an env's 16 lanes (every bearing of an
+    opponent that gets a fix), which config 4's bench line reports; the
+    one-lane kernel pools nothing. Results are unchanged with counters bound."""
+    from lnw import _abi
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    cs = CASES["8v10ls_g200"]
+    grid = load_fixture("grids.npz")["grid200"]
+    E = cs["E"]
+    nb, nr = len(cs["blue"]), len(cs["red"])
+    sc = Scenario(landing_ops=True, auto_reset=True, episode_steps=25)
+    pos = _box_positions(grid, E, nb, nr, 5, cs["box_b"], cs["box_r"])
+    rng = np.random.default_rng(4)
+    acts = [torch.from_numpy(rng.random((E, nb + nr, 4)).astype(np.float32)).cuda() for _ in range(12)]
+    runs = {}
+    for label, count, no_group in (("group", True, False), ("plain", False, False), ("lane", True, True)):
+        if no_group:
+            monkeypatch.setenv("LNW_NO_GROUP", "1")
+        gm = BatchedGame(E, cs["blue"], cs["red"], scenario=sc, grid=grid, seed=11)
+        monkeypatch.delenv("LNW_NO_GROUP", raising=False)
+        gm.reset(positions=pos[0], pos_per_env=torch.from_numpy(pos))
+        if count:
+            gm.count_work(True)
+        traj = []
+        for a in acts:
+            traj.append({k: v.cpu().numpy().copy() for k, v in gm.step(a.clone()).items()})
+            assert gm.step_kernel() == (_abi.KERNEL_GENERIC if no_group else _abi.KERNEL_GROUP)
+        torch.cuda.synchronize()
+        runs[label] = (traj, gm.work_counts() if count else None)
+        gm.close()
+    for s in range(len(acts)):
+        for k in runs["group"][0][s]:
+            assert np.array_equal(runs["group"][0][s][k], runs["plain"][0][s][k], equal_nan=True), (s, k)
+    assert runs["group"][1]["pooled_bearings"] > 0, runs["group"][1]
+    assert runs["lane"][1]["pooled_bearings"] == 0, runs["lane"][1]

@@ -126,10 +126,11 @@ def test_astar_batch_golden(lib, grids):
     for gi in (0, 1):
         m = fx["grid_id"] == gi
         n = int(m.sum())
-        # fixture classes: 0 small (speed 3), 1 ls (speed 2), 2 medium (skip: unsupported type)
+        # fixture classes: 0 small (speed 3), 1 ls (speed 2), 2 medium (speed 2)
         cls = fx["cls"][m]
-        keep = cls != 2
-        types = np.where(cls == 1, 2, 0).astype(np.int8)[keep]
+        keep = np.ones(len(cls), bool)
+        assert gi == 1 or (cls == 2).any()  # the medium cases are there (grid 100)
+        types = np.choose(cls, [0, 2, 3]).astype(np.int8)
         st, tg = fx["start"][m][keep], fx["target"][m][keep]
         k = int(keep.sum())
         plen = torch.zeros(k, dtype=torch.int16, device="cuda")
@@ -147,8 +148,9 @@ def test_astar_batch_golden(lib, grids):
 @pytest.mark.parametrize("move_mode", [0, 1])
 def test_move_table_exhaustive(lib, grids, gi, move_mode):
     """check_path for every start cell x every target offset in [-4,4]^2 (the
-    move table's window) for Combatant and LandingShip: table (move_mode 0) and
-    A* replica (move_mode 1) against the oracle."""
+    move table's window) for Combatant, LandingShip and the medium Combatant
+    (speed 2): table (move_mode 0) and A* replica (move_mode 1) against the
+    oracle."""
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
     grid = grids[gi]
@@ -161,7 +163,7 @@ def test_move_table_exhaustive(lib, grids, gi, move_mode):
     st = np.repeat(cells, 81, axis=0)
     tg = st + np.tile(off, (len(cells), 1))
     n = len(st)
-    for tcode, ocls in ((0, 0), (2, 1)):
+    for tcode, ocls in ((0, 0), (2, 1), (3, 2)):
         _, _, ref = astar_batch(grid, np.full(n, ocls, np.int8), st, tg)
         out = torch.zeros(n, dtype=torch.uint8, device="cuda")
         assert lib.lnw_path_query(g.h, _p(_dev(np.full(n, tcode, np.int8))),
@@ -355,7 +357,8 @@ def test_episode_gpu_tape_contact_variant(name, grids):
 
 
 @pytest.mark.parametrize("name", ["ep_4v4_melee_f64.npz", "ep_4v4_split_f64.npz",
-                                  "ep_8v10ls_g200.npz", "ep_4v4_wild.npz"])
+                                  "ep_8v10ls_g200.npz", "ep_4v4_wild.npz",
+                                  "ep_3v3_medium_melee_observe.npz"])
 def test_episode_gpu_tape_march_astar(name, grids):
     """Same episodes with the LOS ray march and the direct A* instead of the
     precomputed tables."""

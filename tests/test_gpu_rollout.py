@@ -132,10 +132,12 @@ def test_actor_device_matches_reference():
 
 @pytest.mark.parametrize("E,T,contact", [(512, 10, False), (32768, 40, True)])
 def test_rollout_graph_replay_matches_eager(E, T, contact):
-    """Rollout.capture / replay (HIP graph of a whole rollout) against the eager
-    run from the same env state and generator state: identical buffers. The
-    second case is config 5's full size (32 768 envs, 40-step rollout, the
-    contact kernel variant the config-5 bench line uses)."""
+    """Rollout.capture / replay (HIP graph of a whole rollout, fused kernels)
+    against the eager run from the same env state and rollout index: identical
+    buffers. The second case is config 5's full size (32 768 envs, 40-step
+    rollout, the contact kernel variant the config-5 bench line uses). A second
+    replay from the same env state draws fresh actions: the graph advances the
+    device rollout counter the keyed draws read."""
     from lnw import _abi
     from lnw.rollout import BatchedActor, BatchedCritic, Rollout
     g = _game(E, seed=5)
@@ -143,21 +145,124 @@ def test_rollout_graph_replay_matches_eager(E, T, contact):
     torch.manual_seed(2)
     actor = BatchedActor.for_obs(g.Db).cuda()
     critic = BatchedCritic(g.Db * g.nb).cuda()
-    gen = torch.Generator(device="cuda")
-    r = Rollout(g, actor, critic, steps=T, noise=0.05)
-    r.capture(generator=gen)
+    r = Rollout(g, actor, critic, steps=T, noise=0.05, seed=99)
+    r.capture()
     g.reset(positions=REF_BLUE + REF_RED, box=((40, 40), (57, 65)))
-    snap = {f: g.get(f).clone() for f in range(_abi.F_ERR + 1)}  # incl. RNG counters
-    gen.manual_seed(11)
-    eager = {k: v.clone() for k, v in r.run(generator=gen).items() if v is not None}
-    for f, v in snap.items():
-        g.set(f, v)
-    gen.manual_seed(11)
+    snap = g.get_state(device="cuda")  # incl. RNG counters
+    r.call_index(7)
+    eager = {k: v.clone() for k, v in r.run().items() if v is not None}
+    assert r.call_index() == 8
+    g.set_state(snap)
+    r.call_index(7)
     out = r.replay()
     torch.cuda.synchronize()
+    assert r.call_index() == 8
     for k, v in eager.items():
         assert torch.equal(out[k], v), k
+    first = out["actions"][:, 0].clone()
+    g.set_state(snap)
+    out2 = r.replay()  # rollout index 8: other draws from the same observations
+    torch.cuda.synchronize()
+    assert torch.equal(out2["obs"][:, 0], eager["obs"][:, 0])
+    assert not torch.equal(out2["actions"][:, 0], first)
     g.close()
+
+
+def test_torch_impl_keyed_capture_refused():
+    """a captured torch-impl rollout with keyed draws would replay
+    the capture's draws forever; capture() refuses it."""
+    from lnw.rollout import BatchedActor, Rollout
+    g = _game(64)
+    r = Rollout(g, BatchedActor.for_obs(g.Db).cuda(), None, steps=2, impl="torch", keyed_seed=3)
+    with pytest.raises(RuntimeError, match="cannot be captured"):
+        r.capture()
+    g.close()
+
+
+@pytest.mark.parametrize("red", ["script", "actor"])
+def test_fused_rollout_matches_torch_impl(red):
+    """The fused kernels (lnw_policy_act, lnw_rollout_post) against the torch
+    implementation of the same rollout: with forced actor outputs (so both
+    step the same envs) every buffer agrees — observations, actions, running
+    flags, rewards and the row kinds exactly; log-probabilities within 1e-4
+    and values within 1e-5 (float32 network arithmetic in another order).
+    One step of keyed sampling agrees within 1e-5 (the same Philox normals)."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    from lnw.rollout import BatchedActor, BatchedCritic, Rollout
+    E, T = 384, 24
+    sc = Scenario(landing_ops=False, trained_red=red != "script", auto_reset=False)
+    torch.manual_seed(4)
+    actor = BatchedActor.for_obs(68).cuda()
+    critic = BatchedCritic(68 * 4).cuda()
+    red_actor = BatchedActor.for_obs(68).cuda() if red == "actor" else None
+    with torch.no_grad():  # non-trivial running statistics for the red eval mode
+        for m in (actor, red_actor):
+            if m is not None:
+                m.norm1.running_mean.uniform_(-0.2, 0.2)
+                m.norm1.running_var.uniform_(0.5, 2.0)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    forced = torch.rand((E, T, 8, 4), generator=gen, device="cuda")
+    outs = {}
+    for impl in ("hip", "torch"):
+        g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, seed=8, reward_dtype=torch.float64)
+        g.set_variant(True)
+        g.reset(positions=REF_BLUE + REF_RED, box=((40, 40), (57, 65)))
+        r = Rollout(g, actor, critic, steps=T, red=red, red_actor=red_actor, impl=impl)
+        outs[impl] = {k: v.clone() for k, v in r.run(forced_actions=forced).items()}
+        g.close()
+    h, t = outs["hip"], outs["torch"]
+    for k in ("obs", "actions", "running", "rewards", "f32_step", "rtg"):
+        assert torch.equal(h[k], t[k]), k
+    assert not h["running"].all()  # episodes ended inside the rollout: masking exercised
+    torch.testing.assert_close(h["log_probs"], t["log_probs"], rtol=0, atol=1e-4)
+    torch.testing.assert_close(h["values"], t["values"], rtol=0, atol=1e-5)
+    # keyed sampling, one step from the same state
+    samp = {}
+    for impl in ("hip", "torch"):
+        g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, seed=8)
+        g.reset(positions=REF_BLUE + REF_RED, box=((40, 40), (57, 65)))
+        r = Rollout(g, actor, None, steps=1, red=red, red_actor=red_actor, impl=impl, keyed_seed=21,
+                    noise=0.05)
+        samp[impl] = {k: v.clone() for k, v in r.run().items()}
+        g.close()
+    torch.testing.assert_close(samp["hip"]["actions"], samp["torch"]["actions"], rtol=0, atol=1e-5)
+    torch.testing.assert_close(samp["hip"]["log_probs"], samp["torch"]["log_probs"], rtol=0, atol=1e-3)
+
+
+def test_policy_act_direct():
+    """lnw_policy_act on random rows through the C-ABI: means / log-probs of
+    forced actions against the torch actor (get_dist) within 1e-4, NaN rows
+    keep NaN log-probabilities like get_dist."""
+    import ctypes as C
+    from lnw import _abi
+    from lnw.rollout import BatchedActor
+    L = _abi.load()
+    torch.manual_seed(6)
+    a = BatchedActor.for_obs(68).cuda()
+    E, n = 1000, 4
+    obs = torch.rand((E, n, 68), device="cuda")
+    obs[:, :, :49] = torch.randint(0, 256, (E, n, 49), device="cuda") / 255.0
+    act = torch.rand((E, n, 4), device="cuda")
+    alive = torch.ones((n, E), dtype=torch.uint8, device="cuda")
+    alive[2, ::7] = 0
+    lp = torch.zeros((E, n, 4), device="cuda")
+    ao = torch.zeros((E, n, 4), device="cuda")
+    full = torch.zeros((E, n, 4), dtype=torch.float64, device="cuda")
+    params = a.packed_policy()
+    pa = _abi.PolicyArgs()
+    pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = obs.data_ptr(), E, n, 68, 0, n
+    pa.params, pa.forced, pa.forced_act, pa.fa_env_stride = params.data_ptr(), 1, act.data_ptr(), n * 4
+    pa.alive, pa.act_out, pa.logp_out, pa.act_env_stride = alive.data_ptr(), ao.data_ptr(), lp.data_ptr(), n * 4
+    pa.full = full.data_ptr()
+    _abi.check(L.lnw_policy_act(C.byref(pa), None))
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        want, _ = a.get_dist(obs.reshape(E * n, 68), act.reshape(E * n, 4))
+    keep = alive.t().bool()[:, :, None]
+    torch.testing.assert_close(lp, torch.where(keep, want.reshape(E, n, 4), 0.0), rtol=0, atol=1e-4)
+    torch.testing.assert_close(ao, torch.where(keep, act, 0.0), rtol=0, atol=0)
+    torch.testing.assert_close(full, torch.where(keep, act, 0.0).double(), rtol=0, atol=0)
 
 
 def _port():
@@ -194,7 +299,10 @@ def test_rollout_shards_equal_one_rank(tmp_path, red):
     env_id_base = its first global env and keyed sampling, equal one rank over
     all envs bit for bit: observations, actions, log-probabilities, rewards,
     values, running masks and reward-to-go of two consecutive rollouts
-    (auto-reset, melee-box spawns: fire and sinkings)."""
+    (auto-reset, melee-box spawns: fire and sinkings). Bit-exact equality holds
+    because the fused policy kernel computes every row on its own (one thread
+    per row, a fixed operation order), independent of how many rows a rank
+    holds — no GEMM whose kernel choice depends on the batch shape."""
     total = 1024
     one = _rollout_ranks(tmp_path, 1, total, red)[0]
     two = _rollout_ranks(tmp_path, 2, total, red)

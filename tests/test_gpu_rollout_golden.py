@@ -5,7 +5,9 @@ lnw.rollout.Rollout on the device against fixtures recorded from
 Each recorded rollout episode is one device env, replayed in tape mode (every
 random / gauss / randint / beta draw of the reference), with the reference's
 actor / critic / red-actor weights and its sampled actor outputs replayed
-(`forced_actions`; torch's sampler draws are not the env's). Checked per env
+(`forced_actions`; torch's sampler draws are not the env's). Both rollout
+implementations: the fused HIP kernels (lnw_policy_act / lnw_rollout_post) and
+the torch ops. Checked per env
 and step: the observations the actor saw (bit-exact float32), the action
 array's value kind after np.asarray (ppo.py:577), rewards (float64, 1e-5),
 log-probabilities and critic values (float32 network arithmetic on another
@@ -29,9 +31,10 @@ pytestmark = pytest.mark.gpu
 NAMES = {0: "small", 1: "large", 2: "ls"}
 
 
+@pytest.mark.parametrize("impl", ["hip", "torch"])
 @pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact",
                                   "4v4_melee_done"])
-def test_rollout_matches_reference(name):
+def test_rollout_matches_reference(name, impl):
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
     from lnw.rollout import BatchedActor, BatchedCritic, Rollout, gae
@@ -64,7 +67,7 @@ def test_rollout_matches_reference(name):
     if meta["trained_red"]:
         red_actor = BatchedActor.for_obs(g.Dr).load_reference(weights("red_actor.")).cuda()
     r = Rollout(g, actor, critic, steps=T, red="actor" if red_actor is not None else "script",
-                red_actor=red_actor, gamma=meta["gamma"])
+                red_actor=red_actor, gamma=meta["gamma"], impl=impl)
     rng_after = []  # every env's draw counter after each step (the tape position)
     out = r.run(forced_actions=torch.from_numpy(fx["act"]).cuda(),
                 on_step=lambda t, o: rng_after.append(g.env_state()["rng"].copy()))
