@@ -179,6 +179,13 @@ def _main_only(only):
         # before step 40 (done == 0, the `break` at ppo.py:640-641)
         run("4v4_melee_done", n_blue=4, n_red=4, n_ls=0, landing_ops=False, trained_red=True,
             R=8, T=40, seed=34, boxes=(((40, 48), (44, 56)), ((48, 56), (48, 60))))
+    if only is None or "2v2_trained_breaks" in only:
+        # 2v2 fleets 8-20 cells apart, trained red: episodes that run with every
+        # ship alive for a while (float32 action arrays, ppo.py:577) and then end
+        # mid-rollout (done == 0 at steps 7-10: the `break`, ppo.py:640-641),
+        # beside episodes that end at once and ones that reach step 40
+        run("2v2_trained_breaks", n_blue=2, n_red=2, n_ls=0, landing_ops=False, trained_red=True,
+            R=12, T=40, seed=62, boxes=(((37, 43), (45, 53)), ((51, 57), (47, 55))))
 
 
 if __name__ == "__main__":

@@ -33,7 +33,7 @@ NAMES = {0: "small", 1: "large", 2: "ls"}
 
 @pytest.mark.parametrize("impl", ["hip", "torch"])
 @pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact",
-                                  "4v4_melee_done"])
+                                  "4v4_melee_done", "2v2_trained_breaks"])
 def test_rollout_matches_reference(name, impl):
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
@@ -77,6 +77,9 @@ def test_rollout_matches_reference(name, impl):
     assert np.array_equal(run.sum(1), n_steps)
     if name == "4v4_melee_done":  # episodes that end early: the `break` at ppo.py:640-641
         assert (n_steps < T).sum() >= 3, n_steps
+    if name == "2v2_trained_breaks":  # breaks mid-rollout after float32 steps
+        assert ((n_steps >= 5) & (n_steps <= 35)).sum() >= 3, n_steps
+        assert fx["act_f32"].sum() >= 40
     # after an episode's `break` the device buffers hold zeros, like the reference's
     np.testing.assert_array_equal(out["obs"].cpu().numpy(), fx["batch_obs"])
     np.testing.assert_array_equal(out["f32_step"].cpu().numpy() & run, fx["act_f32"].astype(bool))

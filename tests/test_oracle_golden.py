@@ -195,7 +195,7 @@ def test_episode_tlists_golden(name, grids):
 
 
 @pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact",
-                                  "4v4_melee_done"])
+                                  "4v4_melee_done", "2v2_trained_breaks"])
 def test_rollout_fixture_env_trajectory(name, grids):
     """The env side of the recorded reference rollouts (PPO.rollout,
     make_rollout_golden.py) through the oracle: each step observes every live
