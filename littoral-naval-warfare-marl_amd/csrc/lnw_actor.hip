@@ -75,8 +75,9 @@ constexpr int CH_THREADS = 256;
 // The conv head of one row (network.py:70-82): conv 1->5 over the 7x7 window
 // x[0..48] -> BN -> ReLU -> 2x2 pool, conv 5->8 -> BN -> ReLU -> pool, folded
 // into the linear 8->12 (h). P: packed parameters in LDS (broadcast reads);
-// pool1: this workgroup's [45][CH_THREADS] parking area, t: the thread's column.
-__device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pool1, int t,
+// pc: the thread's column of a [45][stride] LDS parking area for the pooled
+// conv1 maps.
+__device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pc, int stride,
                                               bool running, float (&h)[12]) {
   float win[WIN];
 #pragma unroll
@@ -107,42 +108,47 @@ __device__ __forceinline__ void conv_head_row(const float *P, const float *x, fl
 #pragma unroll
       for (int j = 0; j < 3; j++) {
         const int r0 = 2 * i, c0 = 2 * j;
-        pool1[(c * 9 + i * 3 + j) * CH_THREADS + t] =
+        pc[(c * 9 + i * 3 + j) * stride] =
             fmaxf(fmaxf(v[r0 * 7 + c0], v[r0 * 7 + c0 + 1]),
                   fmaxf(v[(r0 + 1) * 7 + c0], v[(r0 + 1) * 7 + c0 + 1]));
       }
   }
-  float p1[45];
-#pragma unroll
-  for (int k = 0; k < 45; k++) p1[k] = pool1[k * CH_THREADS + t];
   // conv2 (5 -> 8, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (3x3 -> 1x1),
-  // folded straight into the linear 8 -> 12 (convhead)
+  // folded straight into the linear 8 -> 12 (convhead). All 8 output maps
+  // accumulate together while the input channels stream in from LDS one at a
+  // time (9 inputs live instead of 45).
+  float v2[8][9];
 #pragma unroll
-  for (int k = 0; k < 12; k++) h[k] = P[HB + k];
+  for (int co = 0; co < 8; co++)
+#pragma unroll
+    for (int p = 0; p < 9; p++) v2[co][p] = P[C2B + co];
 #pragma unroll 1
-  for (int co = 0; co < 8; co++) {
-    float v[9];
+  for (int ci = 0; ci < 5; ci++) {
+    float pin[9];
 #pragma unroll
-    for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 9; k++) pin[k] = pc[(ci * 9 + k) * stride];
 #pragma unroll
-      for (int j = 0; j < 3; j++) {
-        float s = P[C2B + co];
+    for (int co = 0; co < 8; co++) {
+      const float *w = P + C2W + (co * 5 + ci) * 9;
 #pragma unroll
-        for (int ci = 0; ci < 5; ci++) {
-          const float *w = P + C2W + (co * 5 + ci) * 9;
+      for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
 #pragma unroll
           for (int ki = 0; ki < 3; ki++)
 #pragma unroll
             for (int kj = 0; kj < 3; kj++) {
               const int ii = i + ki - 1, jj = j + kj - 1;
-              if (ii >= 0 && ii < 3 && jj >= 0 && jj < 3)
-                s += w[ki * 3 + kj] * p1[ci * 9 + ii * 3 + jj];
+              if (ii >= 0 && ii < 3 && jj >= 0 && jj < 3) v2[co][i * 3 + j] += w[ki * 3 + kj] * pin[ii * 3 + jj];
             }
-        }
-        v[i * 3 + j] = s;
-      }
-    bn_relu<9>(v, P + B2W, P + B2B, P + B2M, P + B2V, co, running);
-    const float f = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[3], v[4]));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 12; k++) h[k] = P[HB + k];
+#pragma unroll
+  for (int co = 0; co < 8; co++) {
+    bn_relu<9>(v2[co], P + B2W, P + B2B, P + B2M, P + B2V, co, running);
+    const float f = fmaxf(fmaxf(v2[co][0], v2[co][1]), fmaxf(v2[co][3], v2[co][4]));
 #pragma unroll
     for (int k = 0; k < 12; k++) h[k] += P[HW + k * 8 + co] * f;
   }
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(CH_THREADS, 2) void features_kernel(const float *pa
        row += (long long)gridDim.x * blockDim.x) {
     const float *x = obs + row * obs_dim;
     float h[12];
-    conv_head_row(P, x, pool1, t, running, h);
+    conv_head_row(P, x, pool1 + t, CH_THREADS, running, h);
     float u[MAX_IN];
     layer_norm_row<MAX_IN>(P, x, n_in, h, u);
     float *o = out + row * n_in;
@@ -220,7 +226,7 @@ constexpr int FC1 = 64, FC2 = 64, FC3 = 32, NOUT = 4;
 struct PolicyArgs {
   lnw_policy_args a;
   int n_in;
-  int off_w1, off_b1, off_w2, off_b2, off_w3, off_b3, off_wm, off_ws;  // packed MLP offsets (floats)
+  int off_b1, off_w1;  // packed MLP: biases b1 | b2 | b3, then the MFMA weight fragments (floats)
 };
 
 __device__ __forceinline__ void philox_u8(unsigned long long seed, unsigned long long ctr0, float (&u)[8]) {
@@ -243,31 +249,77 @@ __device__ __forceinline__ void keyed_eps(unsigned long long seed, unsigned long
   for (int c = 0; c < NOUT; c++) eps[c] = sqrtf(-2.0f * log1pf(-u[c])) * cosf(6.283185307179586f * u[4 + c]);
 }
 
-// tanh(W x + b) of one row for a layer of NO outputs, W row-major [NO][NI]
-// (torch's nn.Linear layout; fc1 zero-padded to NI columns), x in registers,
-// outputs to the thread's LDS column col[o * CH_THREADS]
-template <int NI, int NO>
-__device__ __forceinline__ void dense_layer(cfloat *W, cfloat *b, const float (&x)[NI], float *col) {
-#pragma unroll 1
-  for (int o = 0; o < NO; o += 2) {
-    float a0 = b[o], a1 = b[o + 1];
+// ---- the MLP on the matrix cores -------------------------------------------
+// Each wave runs its 64 rows through fc1 / fc2 / fc3 and the two heads with
+// v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation), transposed:
+// Y^T = W X^T, so the weights are the A operand (lane l: W[n = 16 nt + (l & 15)]
+// [k]) and the activations the B operand (lane l: X[r = 16 rt + (l & 15)][k]),
+// and a layer's output tile (lane l, register v: Y[r = 16 rt + (l & 15)]
+// [n = 16 nt + 4 (l >> 4) + v]) is already the next layer's B operand for the
+// k-steps "quad q = nt, element v" — no LDS round trip between layers. Every
+// layer therefore sums over k in the order k = 16 q + 4 g + v (g = l >> 4), and
+// the host packs each weight matrix as fragments in that order
+// (BatchedActor.packed_policy): float4 [nt][q][lane] = W[16 nt + (lane & 15)]
+// [16 q + 4 (lane >> 4) + 0..3], read with one 16-B load per lane.
+// The first layer's input (the LayerNorm output, one row per lane) goes through
+// a wave-private LDS tile [64 rows][KS] to reach the same layout.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4v mfma4(float a, float b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[rt][nt] += W (frags F, NTO output tiles, Q quads) x X (B operand quads
+// xq[rt][q] of float4 = 4 k-steps)
+template <int NTO, int Q>
+__device__ __forceinline__ void mfma_layer(const f32x4v *__restrict__ F, const f32x4v (&xb)[4][Q],
+                                           f32x4v (&acc)[4][NTO], int lane) {
 #pragma unroll
-    for (int k = 0; k < NI; k++) {
-      a0 = fmaf(W[o * NI + k], x[k], a0);
-      a1 = fmaf(W[(o + 1) * NI + k], x[k], a1);
-    }
-    col[o * CH_THREADS] = tanhf(a0);
-    col[(o + 1) * CH_THREADS] = tanhf(a1);
+  for (int q = 0; q < Q; q++) {
+    f32x4v w[NTO];
+#pragma unroll
+    for (int nt = 0; nt < NTO; nt++) w[nt] = F[(nt * Q + q) * WAVE + lane];
+#pragma unroll
+    for (int v = 0; v < 4; v++)
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int nt = 0; nt < NTO; nt++) acc[rt][nt] = mfma4(w[nt][v], xb[rt][q][v], acc[rt][nt]);
   }
+}
+
+template <int NTO>
+__device__ __forceinline__ void bias_init(const float *__restrict__ b, f32x4v (&acc)[4][NTO], int g) {
+#pragma unroll
+  for (int nt = 0; nt < NTO; nt++) {
+    const f32x4v bv = *(const f32x4v *)(b + nt * 16 + 4 * g);
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) acc[rt][nt] = bv;
+  }
+}
+
+template <int NTO>
+__device__ __forceinline__ void tanh_all(f32x4v (&acc)[4][NTO]) {
+#pragma unroll
+  for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+    for (int nt = 0; nt < NTO; nt++)
+#pragma unroll
+      for (int v = 0; v < 4; v++) acc[rt][nt][v] = tanhf(acc[rt][nt][v]);
 }
 
 template <int NI>
 __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa) {
+  constexpr int Q1 = NI / 16;        // fc1 k-quads (n_in zero-padded to NI)
+  constexpr int KS = NI + 4;         // row stride of the wave's fc1 input tile (16-B aligned)
   const lnw_policy_args &a = pa.a;
   const int n_in = pa.n_in;
   const int n_par = CONV_PARAMS + 2 * n_in;
   float *P = actor_lds;                // [n_par] conv head + LayerNorm parameters
-  float *pool1 = actor_lds + n_par;    // [64][CH_THREADS]: conv1 maps, then the MLP layer columns
+  // per wave: [45][64] pooled conv1 maps (one column per lane), then the
+  // wave's fc1 input tile [64][KS] over the same floats
+  constexpr int WAREA = (45 > KS ? 45 : KS) * WAVE;
+  float *warea = actor_lds + ((n_par + 3) & ~3) + (threadIdx.x / WAVE) * WAREA;
   for (int i = threadIdx.x; i < n_par; i += blockDim.x) P[i] = a.params[i];
   const int n = a.n, D = a.D;
   const long long rows = a.E * n;
@@ -288,15 +340,16 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
     }
   }
   __syncthreads();
+  const int lane = threadIdx.x & (WAVE - 1), g = lane >> 4, m = lane & 15;
   const long long r = r0 + threadIdx.x;
-  if (r >= rows) return;
-  const long long e = r / n;
-  const int i = (int)(r - e * n);
+  const bool valid = r < rows;  // (every lane stays for the wave-wide MFMAs)
+  const long long e = valid ? r / n : 0;
+  const int i = valid ? (int)(r - e * n) : 0;
   const long long E = a.E;
-  const bool alive = a.alive[(long long)(a.own0 + i) * E + e] != 0;
-  const bool live = !a.live || a.live[e] != 0;
+  const bool alive = valid && a.alive[(long long)(a.own0 + i) * E + e] != 0;
+  const bool live = !a.live || (valid && a.live[e] != 0);
   // ---- env-level side work by the lane of ship 0 ---------------------------
-  if (i == 0) {
+  if (valid && i == 0) {
     if (a.script) {  // scripted rows: profile j for red ship j < script_n, zeros past the table
       for (int j = 0; j < a.script_cnt; j++) {
         const int ag = a.script_own0 + j;
@@ -315,44 +368,67 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
       if (a.f32_out) a.f32_out[e * a.f32_env_stride] = k == LNW_KIND_F32 ? 1 : 0;
     }
   }
-  // ---- actor forward --------------------------------------------------------
-  const float *x = a.obs + r * D;
-  float h[12];
-  conv_head_row(P, x, pool1, threadIdx.x, a.bn_running != 0, h);
+  // ---- conv head + LayerNorm, one row per lane -------------------------------
   float u[NI];
-  layer_norm_row<NI>(P, x, n_in, h, u);
-  // MLP: each layer's outputs two at a time (independent FMA chains over the
-  // inputs, held in registers under static indices) with the weights of those
-  // two rows as scalar loads; outputs go to the thread's LDS column (the conv
-  // scratch, dead now) and are read back as the next layer's register inputs.
-  // (Fully unrolled layers had the compiler hoist thousands of scalar weight
-  // loads and spill them.)
-  cfloat *W = (cfloat *)a.params;
-  float *col = pool1 + threadIdx.x;  // [FC1][CH_THREADS]
-  dense_layer<NI, FC1>(W + pa.off_w1, W + pa.off_b1, u, col);
-  float h1[FC1];
+  if (valid) {
+    const float *x = a.obs + r * D;
+    float h[12];
+    conv_head_row(P, x, warea + lane, WAVE, a.bn_running != 0, h);
+    layer_norm_row<NI>(P, x, n_in, h, u);
+  } else {
 #pragma unroll
-  for (int k = 0; k < FC1; k++) h1[k] = col[k * CH_THREADS];
-  dense_layer<FC1, FC2>(W + pa.off_w2, W + pa.off_b2, h1, col);
-  float h2[FC2];
+    for (int k = 0; k < NI; k++) u[k] = 0.f;
+  }
+  // ---- fc1 input tile: the wave's rows into the MFMA B layout ---------------
+  // (over the wave's own conv1 area: its lanes are done with it, and a wave's
+  // LDS operations complete in order)
+  float *xt = warea;
 #pragma unroll
-  for (int k = 0; k < FC2; k++) h2[k] = col[k * CH_THREADS];
-  dense_layer<FC2, FC3>(W + pa.off_w3, W + pa.off_b3, h2, col);
-  float h3[FC3];
+  for (int k4 = 0; k4 < NI / 4; k4++)
+    *(f32x4v *)(xt + lane * KS + 4 * k4) = f32x4v{u[4 * k4], u[4 * k4 + 1], u[4 * k4 + 2], u[4 * k4 + 3]};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  f32x4v xb[4][Q1];
 #pragma unroll
-  for (int k = 0; k < FC3; k++) h3[k] = col[k * CH_THREADS];
+  for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+    for (int q = 0; q < Q1; q++) xb[rt][q] = *(const f32x4v *)(xt + (rt * 16 + m) * KS + 16 * q + 4 * g);
+  // ---- MLP on the matrix cores ----------------------------------------------
+  const f32x4v *Fw = (const f32x4v *)(a.params + pa.off_w1);
+  const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
+  f32x4v h1[4][4];
+  bias_init<4>(bias, h1, g);
+  mfma_layer<4, Q1>(Fw, xb, h1, lane);
+  tanh_all<4>(h1);
+  f32x4v h2[4][4];
+  bias_init<4>(bias + 64, h2, g);
+  mfma_layer<4, 4>(Fw + 4 * Q1 * WAVE, h1, h2, lane);
+  tanh_all<4>(h2);
+  f32x4v h3[4][2];
+  bias_init<2>(bias + 128, h3, g);
+  mfma_layer<2, 4>(Fw + (4 * Q1 + 16) * WAVE, h2, h3, lane);
+  tanh_all<2>(h3);
+  f32x4v hh[4][1];
+#pragma unroll
+  for (int rt = 0; rt < 4; rt++) hh[rt][0] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  mfma_layer<1, 2>(Fw + (4 * Q1 + 24) * WAVE, h3, hh, lane);
+  // head outputs of row 16 rt + m sit in lane m (normal head, n = v) and lane
+  // 16 + m (log-std head, n = 4 + v) of tile rt: bring row `lane` to lane
+  // `lane` (rt = g) for the per-row sampling below
   float mean[NOUT], lsd[NOUT];
 #pragma unroll
-  for (int o = 0; o < NOUT; o++) {
-    float m = 0.f, l = 0.f;
+  for (int v = 0; v < NOUT; v++) {
+    float mv = 0.f, lv = 0.f;
 #pragma unroll
-    for (int k = 0; k < FC3; k++) {
-      m = fmaf(W[pa.off_wm + o * FC3 + k], h3[k], m);
-      l = fmaf(W[pa.off_ws + o * FC3 + k], h3[k], l);
+    for (int rt = 0; rt < 4; rt++) {
+      const float sm = __shfl(hh[rt][0][v], m);
+      const float sl = __shfl(hh[rt][0][v], 16 + m);
+      mv = g == rt ? sm : mv;
+      lv = g == rt ? sl : lv;
     }
-    mean[o] = m;
-    lsd[o] = l;
+    mean[v] = mv;
+    lsd[v] = lv;
   }
+  if (!valid) return;
   float std_[NOUT];
   bool ok = true;
 #pragma unroll
@@ -427,7 +503,9 @@ constexpr int CF1 = 32, CF2 = 64, CF3 = 64;
 __global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_args a, int off_w1, int off_b1,
                                                           int off_w2, int off_b2, int off_w3, int off_b3,
                                                           int off_w4, int off_b4) {
-  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  // (the wave index read through readfirstlane: provably wave-uniform, so the
+  // weight indices below are too and the weights arrive as scalar loads)
+  const int lane = threadIdx.x & (WAVE - 1), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
   const int n = a.n, D = a.D;
   // dynamic LDS: fc1 partials [n][32][65] | fc2 outputs [64][65] | fc4 partial dots [n][64]
   float *part = actor_lds;
@@ -520,11 +598,12 @@ int lnw_actor_features(const float *params_dev, int32_t obs_dim, const float *ob
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 
-// Packed MLP part of lnw_policy_act's parameters, after the conv head block
-// (BatchedActor.packed_policy()), torch's [out][in] layouts: fc1 W [64][K1]
-// (zero-padded to K1 = 32 columns when n_in <= 32, else 64), b [64]; fc2 W
-// [64][64], b [64]; fc3 W [32][64], b [32]; normal head W [4][32]; log-std
-// head W [4][32].
+// Packed MLP part of lnw_policy_act's parameters (BatchedActor.packed_policy()),
+// after the conv head block padded to a multiple of 4 floats: b1 [64], b2 [64],
+// b3 [32], then the MFMA A-operand fragments of fc1 (n_in zero-padded to K1 =
+// 32, or 64 when n_in > 32), fc2, fc3 and the heads (normal rows 0-3, log-std
+// rows 4-7, zero rows to 16), each as float4 [n-tile][k-quad][lane] (see
+// mfma_layer).
 int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   if (!args) return LNW_EINVAL;
   const lnw_policy_args &a = *args;
@@ -546,18 +625,13 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   pa.a = a;
   pa.n_in = a.D - WIN + 12;
   int o = CONV_PARAMS + 2 * pa.n_in;
-  const int k1 = pa.n_in <= 32 ? 32 : MAX_IN;  // fc1 columns as packed (zero-padded)
-  pa.off_w1 = o; o += k1 * FC1;
-  pa.off_b1 = o; o += FC1;
-  pa.off_w2 = o; o += FC1 * FC2;
-  pa.off_b2 = o; o += FC2;
-  pa.off_w3 = o; o += FC2 * FC3;
-  pa.off_b3 = o; o += FC3;
-  pa.off_wm = o; o += FC3 * NOUT;
-  pa.off_ws = o;
+  o = (o + 3) & ~3;     // (16-B aligned biases and fragments)
+  pa.off_b1 = o; o += FC1 + FC2 + FC3;
+  pa.off_w1 = o;
   const long long rows = a.E * a.n;
   const unsigned blocks = (unsigned)((rows + CH_THREADS - 1) / CH_THREADS);
-  const size_t lds = (size_t)(CONV_PARAMS + 2 * pa.n_in + FC1 * CH_THREADS) * sizeof(float);
+  const int npar4 = (CONV_PARAMS + 2 * pa.n_in + 3) & ~3;
+  const size_t lds = (size_t)(npar4 + (CH_THREADS / WAVE) * (pa.n_in <= 32 ? 45 : MAX_IN + 4) * WAVE) * sizeof(float);
   if (pa.n_in <= 32)
     policy_act_kernel<32><<<blocks, CH_THREADS, lds, (hipStream_t)stream>>>(pa);
   else

@@ -80,15 +80,28 @@ class BatchedActor(nn.Module):
 
     def packed_policy(self):
         """Every parameter lnw_policy_act reads (csrc/lnw_actor.hip), in its order:
-        packed_features(), then the MLP in torch's [out][in] layouts: fc1 W
-        zero-padded to 32 columns (64 when n_in > 32), fc1 b, fc2 W, b, fc3 W, b,
-        normal_head W, log_std_head W."""
+        packed_features() zero-padded to a multiple of 4 floats; the biases b1
+        [64], b2 [64], b3 [32]; then the MFMA A-operand fragments of fc1 (n_in
+        zero-padded to 32 columns, 64 when n_in > 32), fc2, fc3 and the heads
+        (normal_head rows 0-3, log_std_head rows 4-7, zero rows to 16), each as
+        float4 [n-tile][k-quad][lane] = W[16 nt + lane % 16][16 q + 4 (lane // 16)
+        + 0..3] (the k order the kernel's chained MFMA layers sum in)."""
         n_in = self.layernorm.normalized_shape[0]
+        dev = self.fc1.weight.device
+
+        def frags(w, k_pad, n_pad):
+            wp = torch.zeros((n_pad, k_pad), dtype=torch.float32, device=dev)
+            wp[:w.shape[0], :w.shape[1]] = w.detach().float()
+            # [nt][m][q][g][v] -> [nt][q][lane = 16 g + m][v]
+            return wp.reshape(n_pad // 16, 16, k_pad // 16, 4, 4).permute(0, 2, 3, 1, 4).reshape(-1)
+
+        conv = self.packed_features()
+        conv = torch.cat([conv, torch.zeros((-conv.numel()) % 4, device=dev)])
         k1 = 32 if n_in <= 32 else 64
-        w1 = torch.zeros((64, k1), dtype=torch.float32, device=self.fc1.weight.device)
-        w1[:, :n_in] = self.fc1.weight.detach().float()
-        parts = [self.packed_features(), w1, self.fc1.bias, self.fc2.weight, self.fc2.bias,
-                 self.fc3.weight, self.fc3.bias, self.normal_head.weight, self.log_std_head.weight]
+        heads = torch.cat([self.normal_head.weight, self.log_std_head.weight], 0)
+        parts = [conv, self.fc1.bias, self.fc2.bias, self.fc3.bias,
+                 frags(self.fc1.weight, k1, 64), frags(self.fc2.weight, 64, 64),
+                 frags(self.fc3.weight, 64, 32), frags(heads, 32, 16)]
         return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
 
     def features(self, obs, bn="sample"):
