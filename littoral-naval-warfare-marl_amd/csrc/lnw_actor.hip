@@ -298,6 +298,15 @@ __device__ __forceinline__ void bias_init(const float *__restrict__ b, f32x4v (&
   }
 }
 
+// tanh(x) = 1 - 2 / (e^(2x) + 1) with the hardware exp2 and reciprocal
+// (v_exp_f32, v_rcp_f32: ~1 ulp each): absolute error below 3e-7 over the
+// whole range (+-1 exactly at overflow), against ~40 instructions of ocml's
+// tanhf. The policy tolerances are 1e-4 (log-probabilities) and 1e-5 (values).
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // e^(2x) = 2^(2x log2 e)
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+
 template <int NTO>
 __device__ __forceinline__ void tanh_all(f32x4v (&acc)[4][NTO]) {
 #pragma unroll
@@ -305,7 +314,7 @@ __device__ __forceinline__ void tanh_all(f32x4v (&acc)[4][NTO]) {
 #pragma unroll
     for (int nt = 0; nt < NTO; nt++)
 #pragma unroll
-      for (int v = 0; v < 4; v++) acc[rt][nt][v] = tanhf(acc[rt][nt][v]);
+      for (int v = 0; v < 4; v++) acc[rt][nt][v] = tanh_fast(acc[rt][nt][v]);
 }
 
 template <int NI>
@@ -373,7 +382,11 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   if (valid) {
     const float *x = a.obs + r * D;
     float h[12];
+#ifdef LNW_PROBE_NOCONV  // timing probes only (tools/policy_probe.py): no conv head
+    for (int k = 0; k < 12; k++) h[k] = x[k];
+#else
     conv_head_row(P, x, warea + lane, WAVE, a.bn_running != 0, h);
+#endif
     layer_norm_row<NI>(P, x, n_in, h, u);
   } else {
 #pragma unroll
@@ -393,6 +406,10 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
 #pragma unroll
     for (int q = 0; q < Q1; q++) xb[rt][q] = *(const f32x4v *)(xt + (rt * 16 + m) * KS + 16 * q + 4 * g);
   // ---- MLP on the matrix cores ----------------------------------------------
+#ifdef LNW_PROBE_NOMLP  // timing probes only: no MLP
+  float mean[NOUT], lsd[NOUT];
+  for (int v = 0; v < NOUT; v++) { mean[v] = xb[0][0][v]; lsd[v] = 0.f; }
+#else
   const f32x4v *Fw = (const f32x4v *)(a.params + pa.off_w1);
   const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
   f32x4v h1[4][4];
@@ -428,6 +445,7 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
     mean[v] = mv;
     lsd[v] = lv;
   }
+#endif
   if (!valid) return;
   float std_[NOUT];
   bool ok = true;
@@ -489,85 +507,129 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
 // ---------------------------------------------------------------------------
 // After lnw_step (lnw_rollout_post): the rollout's bookkeeping of step t and
 // the critic (network.py:154-172, ppo.py:598-605) on the observations the actor
-// saw (the rollout buffer at step t). One workgroup = 64 envs x n waves, wave w
-// = ship w, lane = env:
-//   fc1: wave w sums ship w's D inputs into partial sums of all 32 outputs
-//        (LDS), then every wave adds the n partials and the bias (tanh);
-//   fc2 / fc3: the 64 outputs split over the waves, exchanged through LDS;
-//   fc4: per-wave partial dots, summed by wave 0;
-//   wave 0 then stores the value (0 after the episode ended), the rewards, the
-//   running flag and the env's new live flag (done == 0 ends it, ppo.py:640).
+// saw (the rollout buffer at step t), on the matrix cores like the actor's MLP
+// (v_mfma_f32_16x16x4_f32, transposed layers Y^T = W X^T, k order 16 q + 4 g +
+// v; see mfma_layer). One workgroup = 64 envs (4 row tiles) x n waves:
+//   fc1 (n D -> 32): wave w takes ship w's D inputs (zero-padded to DQ
+//        quads), partial sums of all 32 outputs for the 64 envs, added up
+//        through LDS by every wave (+ bias, tanh);
+//   fc2 (32 -> 64) and fc3 (64 -> 64): the 16-output tiles dealt over the
+//        waves, fc2's tiles exchanged through LDS in the MFMA operand layout;
+//   fc4 (64 -> 1): each wave's fc3 tiles dotted with w4 in registers, summed
+//        over lane groups (shuffles) and waves (LDS);
+//   wave 0, lane = env: the value (0 after the episode ended), the rewards,
+//   the running flag and the env's new live flag (done == 0 ends it, ppo.py:640).
+// Packed critic (BatchedCritic.packed()): fc1 fragments per ship [n][2][DQ]
+// [lane] float4, b1 [32], fc2 fragments [4][2][lane], b2 [64], fc3 fragments
+// [4][4][lane], b3 [64], w4 [64], b4 (+ 3 zeros).
 // ---------------------------------------------------------------------------
 constexpr int CF1 = 32, CF2 = 64, CF3 = 64;
 
-__global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_args a, int off_w1, int off_b1,
-                                                          int off_w2, int off_b2, int off_w3, int off_b3,
-                                                          int off_w4, int off_b4) {
-  // (the wave index read through readfirstlane: provably wave-uniform, so the
-  // weight indices below are too and the weights arrive as scalar loads)
-  const int lane = threadIdx.x & (WAVE - 1), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+struct CriticOffsets { int w1, b1, w2, b2, w3, b3, w4, b4; };
+
+__global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_args a, CriticOffsets co, int dq) {
+  const int lane = threadIdx.x & (WAVE - 1), g = lane >> 4, m = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
   const int n = a.n, D = a.D;
-  // dynamic LDS: fc1 partials [n][32][65] | fc2 outputs [64][65] | fc4 partial dots [n][64]
-  float *part = actor_lds;
-  float *h2s = part + n * CF1 * (WAVE + 1);
-  float *dsum = h2s + CF2 * (WAVE + 1);
-  const long long e = (long long)blockIdx.x * WAVE + lane;
+  const long long e0 = (long long)blockIdx.x * WAVE;
+  const long long e = e0 + lane;
   const bool valid = e < a.E;
   const bool crit = a.critic != nullptr;
-  cfloat *C = (cfloat *)a.critic;
+  // dynamic LDS: fc1 partials [n][2 nt][4 rt][64] f32x4 | fc2 tiles [4][4 rt][64] f32x4 | fc4 dots [n][64]
+  f32x4v *part = (f32x4v *)actor_lds;
+  f32x4v *h2s = part + n * 8 * WAVE;
+  float *dsum = (float *)(h2s + 16 * WAVE);
   if (crit) {
-    float acc[CF1];
+    const float *C = a.critic;
+    // ---- fc1: ship w's inputs --------------------------------------------------
+    f32x4v acc[4][2];
 #pragma unroll
-    for (int o = 0; o < CF1; o++) acc[o] = 0.f;
-    if (valid) {
-      const float *x = a.obs + e * a.obs_env_stride + (long long)w * D;
-      const int kb = w * D;
-      for (int k4 = 0; k4 < D; k4 += 4) {
-        const f32x4 xv = *(const f32x4 *)(x + k4);
+    for (int rt = 0; rt < 4; rt++) acc[rt][0] = acc[rt][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const f32x4v *F1 = (const f32x4v *)(C + co.w1) + (size_t)w * 2 * dq * WAVE;
+    for (int q = 0; q < dq; q++) {  // (uniform trip count; MFMAs unrolled inside)
+      const int k = 16 * q + 4 * g;
+      f32x4v xb[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const float xk = xv[q];
+      for (int rt = 0; rt < 4; rt++) {
+        const long long er = e0 + rt * 16 + m;
+        xb[rt] = (k < D && er < a.E) ? *(const f32x4v *)(a.obs + er * a.obs_env_stride + (long long)w * D + k)
+                                      : f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+      const f32x4v w0 = F1[(0 * dq + q) * WAVE + lane], w1 = F1[(1 * dq + q) * WAVE + lane];
 #pragma unroll
-          for (int o = 0; o < CF1; o++) acc[o] = fmaf(C[off_w1 + (kb + k4 + q) * CF1 + o], xk, acc[o]);
+      for (int v = 0; v < 4; v++)
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++) {
+          acc[rt][0] = mfma4(w0[v], xb[rt][v], acc[rt][0]);
+          acc[rt][1] = mfma4(w1[v], xb[rt][v], acc[rt][1]);
         }
+    }
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++) part[((w * 2 + nt) * 4 + rt) * WAVE + lane] = acc[rt][nt];
+    __syncthreads();
+    f32x4v h1[4][2];
+    bias_init<2>(C + co.b1, h1, g);
+    for (int v = 0; v < n; v++)
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) h1[rt][nt] += part[((v * 2 + nt) * 4 + rt) * WAVE + lane];
+    tanh_all<2>(h1);
+    // ---- fc2: tiles w, w + n, ... ------------------------------------------
+    for (int nt = w; nt < 4; nt += n) {
+      f32x4v t2[4][1];
+      const f32x4v bv = *(const f32x4v *)(C + co.b2 + nt * 16 + 4 * g);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) t2[rt][0] = bv;
+      mfma_layer<1, 2>((const f32x4v *)(C + co.w2) + nt * 2 * WAVE, h1, t2, lane);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) {
+#pragma unroll
+        for (int v = 0; v < 4; v++) t2[rt][0][v] = tanh_fast(t2[rt][0][v]);
+        h2s[(nt * 4 + rt) * WAVE + lane] = t2[rt][0];
       }
     }
-#pragma unroll
-    for (int o = 0; o < CF1; o++) part[(w * CF1 + o) * (WAVE + 1) + lane] = acc[o];
     __syncthreads();
-    float h1[CF1];
+    // ---- fc3 + fc4 partial dots ----------------------------------------------
+    f32x4v h2[4][4];
 #pragma unroll
-    for (int o = 0; o < CF1; o++) {
-      float s = C[off_b1 + o];
-      for (int v = 0; v < n; v++) s += part[(v * CF1 + o) * (WAVE + 1) + lane];
-      h1[o] = tanhf(s);
-    }
-    // fc2: outputs o = w, w + n, ... (wave-uniform weights)
-    for (int o = w; o < CF2; o += n) {
-      float s = C[off_b2 + o];
+    for (int rt = 0; rt < 4; rt++)
 #pragma unroll
-      for (int k = 0; k < CF1; k++) s = fmaf(C[off_w2 + k * CF2 + o], h1[k], s);
-      h2s[o * (WAVE + 1) + lane] = tanhf(s);
-    }
-    __syncthreads();
-    float dot = 0.f;
-    for (int o = w; o < CF3; o += n) {
-      float s = C[off_b3 + o];
+      for (int q = 0; q < 4; q++) h2[rt][q] = h2s[(q * 4 + rt) * WAVE + lane];
+    float dot[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int nt = w; nt < 4; nt += n) {
+      f32x4v t3[4][1];
+      const f32x4v bv = *(const f32x4v *)(C + co.b3 + nt * 16 + 4 * g);
 #pragma unroll
-      for (int k = 0; k < CF2; k++) s = fmaf(C[off_w3 + k * CF3 + o], h2s[k * (WAVE + 1) + lane], s);
-      dot = fmaf(C[off_w4 + o], tanhf(s), dot);
+      for (int rt = 0; rt < 4; rt++) t3[rt][0] = bv;
+      mfma_layer<1, 4>((const f32x4v *)(C + co.w3) + nt * 4 * WAVE, h2, t3, lane);
+      const f32x4v w4 = *(const f32x4v *)(C + co.w4 + nt * 16 + 4 * g);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int v = 0; v < 4; v++) dot[rt] = fmaf(w4[v], tanh_fast(t3[rt][0][v]), dot[rt]);
     }
-    dsum[w * WAVE + lane] = dot;
+    // lane groups g hold outputs 4 g .. 4 g + 3 of each tile: sum over g
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) {
+      dot[rt] += __shfl_xor(dot[rt], 16);
+      dot[rt] += __shfl_xor(dot[rt], 32);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) dsum[w * WAVE + rt * 16 + m] = dot[rt];
+    }
     __syncthreads();
   }
   if (w != 0 || !valid) return;
   const bool L = !a.live || a.live[e] != 0;
   const bool masked = a.stop_at_done != 0;
   if (crit) {
-    float v = C[off_b4];
     float s = 0.f;
     for (int q = 0; q < n; q++) s += dsum[q * WAVE + lane];
-    v += s;
+    const float v = a.critic[co.b4] + s;
     a.val[e * a.val_env_stride] = (masked && !L) ? 0.0f : v;
   }
   if (a.rew && a.rew_out) {
@@ -639,29 +701,30 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 
-// Packed critic (BatchedCritic.packed()): fc1 W^T [in][32], b [32]; fc2 W^T
-// [32][64], b [64]; fc3 W^T [64][64], b [64]; fc4 w [64], b [1]; in = n * D.
+// Packed critic: see rollout_post_kernel (BatchedCritic.packed()).
 int lnw_rollout_post(const lnw_rollout_post_args *args, void *stream) {
   if (!args) return LNW_EINVAL;
   const lnw_rollout_post_args &a = *args;
   if (a.n <= 0 || a.n > 16 || a.E < 0) return LNW_EINVAL;
-  if (a.critic && (!a.obs || !a.val || (a.D & 3) || ((uintptr_t)a.obs & 15) || (a.obs_env_stride & 3)))
+  if (a.critic && (!a.obs || !a.val || (a.D & 3) || ((uintptr_t)a.obs & 15) || (a.obs_env_stride & 3) ||
+                   ((uintptr_t)a.critic & 15)))
     return LNW_EINVAL;
   if (a.rew_out && (!a.rew || a.n_rew <= 0)) return LNW_EINVAL;
   if (a.E == 0) return 0;
-  const int in = a.n * a.D;
+  const int dq = (a.D + 15) / 16;
+  CriticOffsets co;
   int o = 0;
-  const int w1 = o; o += in * CF1;
-  const int b1 = o; o += CF1;
-  const int w2 = o; o += CF1 * CF2;
-  const int b2 = o; o += CF2;
-  const int w3 = o; o += CF2 * CF3;
-  const int b3 = o; o += CF3;
-  const int w4 = o; o += CF3;
-  const int b4 = o;
+  co.w1 = o; o += a.n * 2 * dq * WAVE * 4;
+  co.b1 = o; o += CF1;
+  co.w2 = o; o += 4 * 2 * WAVE * 4;
+  co.b2 = o; o += CF2;
+  co.w3 = o; o += 4 * 4 * WAVE * 4;
+  co.b3 = o; o += CF3;
+  co.w4 = o; o += CF3;
+  co.b4 = o;
   const unsigned blocks = (unsigned)((a.E + WAVE - 1) / WAVE);
-  const size_t lds = a.critic ? (size_t)(a.n * CF1 * (WAVE + 1) + CF2 * (WAVE + 1) + a.n * WAVE) * sizeof(float) : 0;
-  rollout_post_kernel<<<blocks, WAVE * a.n, lds, (hipStream_t)stream>>>(a, w1, b1, w2, b2, w3, b3, w4, b4);
+  const size_t lds = a.critic ? (size_t)(a.n * 8 * WAVE + 16 * WAVE) * 16 + (size_t)a.n * WAVE * 4 : 0;
+  rollout_post_kernel<<<blocks, WAVE * a.n, lds, (hipStream_t)stream>>>(a, co, dq);
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 

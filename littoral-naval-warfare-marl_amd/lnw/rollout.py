@@ -186,12 +186,26 @@ class BatchedCritic(nn.Module):
         self.load_state_dict({k: torch.as_tensor(np.asarray(v)) for k, v in state_dict.items()})
         return self
 
-    def packed(self):
-        """Parameters in lnw_rollout_post's order (csrc/lnw_actor.hip): fc1 W^T
-        [in][32], b; fc2 W^T [32][64], b; fc3 W^T [64][64], b; fc4 w [64], b."""
-        parts = [self.fc1.weight.t(), self.fc1.bias, self.fc2.weight.t(), self.fc2.bias,
-                 self.fc3.weight.t(), self.fc3.bias, self.fc4.weight, self.fc4.bias]
-        return torch.cat([p.detach().contiguous().reshape(-1).float() for p in parts]).contiguous()
+    def packed(self, n_ships, obs_dim):
+        """Parameters in lnw_rollout_post's order (csrc/lnw_actor.hip): the MFMA
+        A-operand fragments of fc1 per ship (its obs_dim inputs zero-padded to
+        a multiple of 16), b1; fc2 fragments, b2; fc3 fragments, b3; fc4 w
+        [64], b (+ 3 zeros). Fragments: float4 [n-tile][k-quad][lane] =
+        W[16 nt + lane % 16][16 q + 4 (lane // 16) + 0..3] (BatchedActor.packed_policy)."""
+        dev = self.fc1.weight.device
+
+        def frags(w, k_pad, n_pad):
+            wp = torch.zeros((n_pad, k_pad), dtype=torch.float32, device=dev)
+            wp[:w.shape[0], :w.shape[1]] = w.detach().float()
+            return wp.reshape(n_pad // 16, 16, k_pad // 16, 4, 4).permute(0, 2, 3, 1, 4).reshape(-1)
+
+        dq = (obs_dim + 15) // 16
+        w1 = self.fc1.weight.detach().float().reshape(32, n_ships, obs_dim)
+        f1 = torch.cat([frags(w1[:, i], 16 * dq, 32) for i in range(n_ships)])
+        parts = [f1, self.fc1.bias, frags(self.fc2.weight, 32, 64), self.fc2.bias,
+                 frags(self.fc3.weight, 64, 64), self.fc3.bias, self.fc4.weight.reshape(-1),
+                 self.fc4.bias, torch.zeros(3, device=dev)]
+        return torch.cat([p.detach().reshape(-1).float() for p in parts]).contiguous()
 
     def forward(self, x):
         x = torch.flatten(x, 1)
@@ -401,7 +415,7 @@ class Rollout:
         live = torch.ones(E, dtype=torch.bool, device=dev)
         red_actor_rows = self.red != "script" and self.red_actor is not None
         ap = self.actor.packed_policy()
-        cp = self.critic.packed() if self.critic is not None else None
+        cp = self.critic.packed(nb, Db) if self.critic is not None else None
         rap = self.red_actor.packed_policy() if red_actor_rows else None
         fa = None
         if forced_actions is not None:
