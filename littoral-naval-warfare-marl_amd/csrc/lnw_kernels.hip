@@ -2239,6 +2239,109 @@ __device__ __forceinline__ void emit_rows_t(const KParams &P, const KState &S, c
   }
 }
 
+// 4-ship sides (D = 68 floats = 17 float4 chunks per row, 68 chunks = 17 whole
+// 64-B lines per env block): rows of one agent leave line-aligned. Row kl
+// spans chunks [17 kl, 17 kl + 17) of the env's block, so rows 0-2 end inside a
+// line the next row finishes; stored as is, every such line is written twice,
+// in two partial pieces (the melee step's WRITE_SIZE was 1.19x the algorithmic
+// bytes). Pass kl instead emits the whole lines [16 kl, 16 kl + 16) (pass 3:
+// [48, 68)): the kl chunks row kl-1 left over (carried in registers) and the
+// first 16 - kl chunks of row kl; its last kl + 1 chunks wait for the next
+// pass. Same values, same addresses, every line written once, whole.
+template <int KL>
+__device__ __forceinline__ void emit_rows_al4_t(const KParams &P, const KState &S, const Cols &c,
+                                                const double *duct_col, int a, float *obs_side, int env0,
+                                                f32x4 (&v)[12], float &w48, f32x4 (&carry)[3]) {
+  constexpr int NS = 4, D4 = 17, T = 4 * NS + 3;
+  constexpr int DC = KL;                          // chunks carried from row KL - 1
+  constexpr int W = KL < NS - 1 ? 16 : 20;        // chunks this pass stores (whole lines)
+  constexpr int NOWN = W - DC;                    // row KL's chunks stored now: 0 .. NOWN - 1
+  constexpr int NDEF = KL < NS - 1 ? D4 - NOWN : 0;  // row KL's chunks left for the next pass
+  constexpr int GS = W / 4;                       // chunks per stage group (4 groups)
+  static_assert(GS <= EST4 && NDEF <= 3, "stage / carry sizes");
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int el = lane;
+  const int own0 = a >= NS ? NS : 0;
+  const float *xg = c.estage + WAVE * EST4 * 4;
+  const uint32_t p = c.pos_cur[a * PAD + el];
+  const int tk = c.type[a * PADB + el];
+  const int alive = c.alive0[a * PADB + el];
+  const int rad = c.radar_cur[a * PAD + el];
+  const int mis = c.miss_cur[a * PADB + el];
+  const uint32_t tcn = c.tcnt[a * PAD + el];
+  const double du = duct_col[el];
+  float t[T];
+  t[0] = xg[pos_x(p)];
+  t[1] = xg[pos_y(p)];
+  t[2] = (float)rad;
+  t[3] = (float)mis * (tk == T_SMALL ? 0.25f : 0.125f);
+#pragma unroll
+  for (int s = 0; s < NS - 1; s++) {
+    const bool nw = s < KL;
+    const int i = own0 + (nw ? s : s + 1);
+    const uint32_t q = (nw ? c.pos_cur : c.pos_old)[i * PAD + el];
+    const int ta = c.alive0[i * PADB + el];
+    const int m = (nw ? c.miss_cur : c.miss_old)[i * PADB + el];
+    const float fm = (float)m * (c.type[i * PADB + el] == T_SMALL ? 0.25f : 0.125f);
+    t[4 + 4 * s] = ta ? xg[pos_x(q)] : 0.0f;
+    t[5 + 4 * s] = ta ? xg[pos_y(q)] : 0.0f;
+    t[6 + 4 * s] = ta ? (float)(nw ? c.radar_cur : c.radar_old)[i * PAD + el] : 0.0f;
+    t[7 + 4 * s] = ta ? fm : 0.0f;
+  }
+  t[T - 3] = (float)tcn;
+  t[T - 2] = tk == T_LS ? 1.0f : 0.0f;
+  t[T - 1] = (float)(du / 2.0);
+  const bool ls = tk == T_LS;
+  f32x4 vc[12];
+#pragma unroll
+  for (int q = 0; q < 12; q++) vc[q] = v[q];
+  const float wc = w48;
+  if (a + 1 < 2 * NS) load_window(S, window_rec(P, c, a + 1, el), v, w48);
+  auto chunk = [&](int q) {  // row chunk q (compile-time q after unrolling)
+    f32x4 o;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const int j = 4 * q + w;
+      const float wv = j < 48 ? vc[j >> 2][j & 3] : (j == 48 ? wc : 0.0f);
+      const float xc = j < 49 ? wv : t[j - 49 < T ? j - 49 : 0];
+      const float xl = j < 25 ? wv : (j - 25 < T ? t[j - 25 < T ? j - 25 : 0] : 0.0f);
+      o[w] = alive ? (ls ? xl : xc) : 0.0f;
+    }
+    return o;
+  };
+  f32x4 *st4 = (f32x4 *)c.estage;
+  f32x4 *out4 = (f32x4 *)obs_side + (size_t)env0 * NS * D4;  // the first env's block
+  constexpr int LS0 = (D4 * KL) & ~3;                         // the pass's first chunk (line start)
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+#pragma unroll
+    for (int u = 0; u < GS; u++) {
+      const int j = g * GS + u;
+      st4[lane * EST4 + u] = j < DC ? carry[j < DC ? j : 0] : chunk(j - DC);
+    }
+    wave_lds_sync();
+    f32x4 cv[EST4];
+#pragma unroll
+    for (int it = 0; it < GS; it++) {
+      const int i = it * WAVE + lane;
+      const int r = i / GS, cc = i - (i / GS) * GS;
+      cv[it] = st4[r * EST4 + cc];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int it = 0; it < GS; it++) {
+      const int i = it * WAVE + lane;
+      const int r = i / GS, cc = i - (i / GS) * GS;
+      const uint32_t i4 = (uint32_t)(r * NS * D4 + LS0 + g * GS + cc);
+      if (P.dbg_skip & 32) continue;
+      if (P.dbg_skip & 64) out4[i4] = cv[it];
+      else st_obs4(out4, i4, cv[it], P.store_wt);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < NDEF; d++) carry[d] = chunk(NOWN + d);
+}
+
 // Wave 1 of a templated step workgroup: emits agent a's rows once wave 0 has
 // published progress > a (LDS counter, -1 until phase S starts: the emission
 // stage aliases the terrain mask phase M reads). Its stores count on its own
@@ -2267,6 +2370,27 @@ __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, c
   float w48;
   load_window(S, window_rec(P, c, 0, lane), v, w48);
   int done = 0;
+  if constexpr (NS == 4) {
+    if (!(P.dbg_skip & 8192)) {  // (diagnostics: bit 13 keeps the row-piece emission)
+      // line-aligned passes (emit_rows_al4_t): the compile-time pass index keeps
+      // the carried chunks in registers
+#pragma unroll 1
+      for (int sd = 0; sd < 2; sd++) {
+        float *out = sd ? obs_r : obs_b;
+        f32x4 carry[3];
+        const int a0 = sd * NS;
+        if (done <= a0) done = wait_progress(prog, a0 + 1);
+        emit_rows_al4_t<0>(P, S, c, duct_col, a0, out, env0, v, w48, carry);
+        if (done <= a0 + 1) done = wait_progress(prog, a0 + 2);
+        emit_rows_al4_t<1>(P, S, c, duct_col, a0 + 1, out, env0, v, w48, carry);
+        if (done <= a0 + 2) done = wait_progress(prog, a0 + 3);
+        emit_rows_al4_t<2>(P, S, c, duct_col, a0 + 2, out, env0, v, w48, carry);
+        if (done <= a0 + 3) done = wait_progress(prog, a0 + 4);
+        emit_rows_al4_t<3>(P, S, c, duct_col, a0 + 3, out, env0, v, w48, carry);
+      }
+      return;
+    }
+  }
   for (int a = 0; a < 2 * NS; a++) {
     if (done <= a) done = wait_progress(prog, a + 1);
     emit_rows_t<NS>(P, S, c, duct_col, a, a >= NS ? obs_r : obs_b, env0, v, w48);
@@ -3708,6 +3832,9 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
   // LNW_NO_XCD_REMAP: workgroup b steps env chunk b (A/B tests of xcd_chunk)
   h->kp.xcd_remap = getenv("LNW_NO_XCD_REMAP") == nullptr ? 1 : 0;
+  // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
+  // terrain mask instead of loading LOS-table words (A/B)
+  h->kp.group_march = getenv("LNW_GROUP_MARCH") != nullptr ? 1 : 0;
   // write-through observation stores (st_obs4) while a side's output fits the
   // 32-bit buffer offsets; LNW_NO_STORE_WT keeps non-temporal stores (A/B)
   {

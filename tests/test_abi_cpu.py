@@ -62,3 +62,15 @@ def test_product_path_has_no_cpu_fallback(tmp_path):
         _abi._lib = None
         _abi.load(str(tmp_path / "missing.so"))
     _abi._lib = None
+
+
+def test_policy_entry_points_validate_arguments(L):
+    """lnw_policy_act / lnw_rollout_post reject malformed arguments before
+    touching the device (no GPU needed)."""
+    assert L.lnw_policy_act(None, None) == -1
+    assert L.lnw_rollout_post(None, None) == -1
+    pa = _abi.PolicyArgs()  # no obs / params / alive
+    assert L.lnw_policy_act(ctypes.byref(pa), None) == -1
+    pp = _abi.RolloutPostArgs()
+    pp.n = 0
+    assert L.lnw_rollout_post(ctypes.byref(pp), None) == -1

@@ -21,8 +21,8 @@ def _oracle_for(game):
     return o
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_facade_rollout_matches_oracle(seed, tmp_path, monkeypatch):
+@pytest.mark.parametrize("seed,blue_type", [(0, "small"), (1, "small"), (2, "small"), (3, "medium")])
+def test_facade_rollout_matches_oracle(seed, blue_type, tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)  # no config.json / PNG here: defaults + packaged grid
     from lnw.game import Game, ShipSpec
     random.seed(seed)
@@ -30,7 +30,7 @@ def test_facade_rollout_matches_oracle(seed, tmp_path, monkeypatch):
     g = Game()
     g.scenario.landing_ops = False
     g.scenario.n_red_landingship = 0
-    blue = [ShipSpec("blue", "small", p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
+    blue = [ShipSpec("blue", blue_type, p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
     red = [ShipSpec("red", "large", p) for p in [(58, 55), (60, 60), (62, 52), (57, 64)]]
     state = random.getstate()
     g.reset(4, 4, blue_ships=blue, red_ships=red)
@@ -39,7 +39,11 @@ def test_facade_rollout_matches_oracle(seed, tmp_path, monkeypatch):
     seed63 = random.getrandbits(63)
     o = _oracle_for(g)
     o.set_philox(seed63, 0)
-    o.reset([0] * 4 + [1] * 4, [s.position for s in blue + red])
+    o.reset([_oracle.T_MEDIUM if blue_type == "medium" else 0] * 4 + [1] * 4,
+            [s.position for s in blue + red])
+    if blue_type == "medium":  # a side of medium ships: 5x5 windows, rows of 4n + 28 (game.py:609)
+        assert g.observation_space == 4 * 4 + 28 and g.red_observation_space == 4 * 4 + 52
+        assert all(s.speed == 2 for s in g.blue_ships)
     o.set_ducting(g.ducting_factor)
     rng = np.random.default_rng(seed)
     for step in range(25):
@@ -97,7 +101,7 @@ def test_facade_analytics_side_channels(tmp_path, monkeypatch):
     g = Game()
     g.scenario.landing_ops = False
     g.scenario.n_red_landingship = 0
-    blue = [ShipSpec("blue", "small", p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
+    blue = [ShipSpec("blue", blue_type, p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
     red = [ShipSpec("red", "large", p) for p in [(58, 55), (60, 60), (62, 52), (57, 64)]]
     rng = np.random.default_rng(4)
     for ep in range(6):

@@ -132,3 +132,79 @@ def test_red_script_table():
     a = red_script_actions(tab, 5, 4)
     assert torch.equal(a[:3], tab[:, 5]) and torch.equal(a[3], torch.zeros(4))
     assert torch.equal(red_script_actions(tab, 40, 2), torch.zeros(2, 4))
+
+
+def _unpack_frags(F, nto, q):
+    """The weight matrix a run of MFMA A-operand fragments encodes: float4
+    [nt][q][lane] = W[16 nt + lane % 16][16 q + 4 (lane // 16) + v]."""
+    import numpy as np
+    fr = np.asarray(F[:nto * q * 256]).reshape(nto, q, 64, 4)
+    W = np.zeros((16 * nto, 16 * q))
+    for lane in range(64):
+        m, g = lane % 16, lane // 16
+        for v in range(4):
+            W[np.arange(nto)[:, None] * 16 + m, np.arange(q)[None, :] * 16 + 4 * g + v] = fr[:, :, lane, v]
+    return W, nto * q * 256
+
+
+def test_policy_packing_matches_layers():
+    """BatchedActor.packed_policy / BatchedCritic.packed (the layouts
+    lnw_policy_act / lnw_rollout_post read): the fragment runs decode back to
+    the torch layers' weights, zero-padded, and a forward pass computed from
+    the decoded arrays equals the torch heads / critic (CPU, no GPU needed)."""
+    import numpy as np
+    import torch
+    from lnw.rollout import BatchedActor, BatchedCritic
+    torch.manual_seed(5)
+    for D, nb in ((68, 4), (60, 2)):
+        a = BatchedActor.for_obs(D)
+        n_in = D - 49 + 12
+        P = a.packed_policy().numpy()
+        conv = (578 + 2 * n_in + 3) // 4 * 4
+        b = P[conv:conv + 160]
+        F = P[conv + 160:]
+        k1 = 32 if n_in <= 32 else 64
+        W1, o = _unpack_frags(F, 4, k1 // 16)
+        W2, o2 = _unpack_frags(F[o:], 4, 4)
+        W3, o3 = _unpack_frags(F[o + o2:], 2, 4)
+        WH, o4 = _unpack_frags(F[o + o2 + o3:], 1, 2)
+        assert o + o2 + o3 + o4 == len(F)
+        assert np.array_equal(W1[:, :n_in], a.fc1.weight.detach().numpy()) and not W1[:, n_in:].any()
+        assert np.array_equal(W2, a.fc2.weight.detach().numpy())
+        assert np.array_equal(W3, a.fc3.weight.detach().numpy())
+        assert np.array_equal(WH[:4], a.normal_head.weight.detach().numpy())
+        assert np.array_equal(WH[4:8], a.log_std_head.weight.detach().numpy()) and not WH[8:].any()
+        x = torch.rand(16, D)
+        with torch.no_grad():
+            feats = a.features(x).numpy()
+            mean, std = a.heads(x)
+        h = np.tanh(feats @ W1[:, :n_in].T + b[:64])
+        h = np.tanh(h @ W2.T + b[64:128])
+        h = np.tanh(h @ W3.T + b[128:160])
+        hh = h @ WH.T
+        np.testing.assert_allclose(np.tanh(hh[:, :4]), mean.numpy(), atol=1e-5)
+        np.testing.assert_allclose(np.exp(hh[:, 4:8]), std.numpy(), rtol=1e-5)
+        c = BatchedCritic(D * nb)
+        C = c.packed(nb, D).numpy()
+        dq = (D + 15) // 16
+        o = 0
+        W1s = []
+        for i in range(nb):
+            w, k = _unpack_frags(C[o:], 2, dq)
+            W1s.append(w[:, :D])
+            assert not w[:, D:].any()
+            o += k
+        b1 = C[o:o + 32]; o += 32
+        W2c, k = _unpack_frags(C[o:], 4, 2); o += k
+        b2 = C[o:o + 64]; o += 64
+        W3c, k = _unpack_frags(C[o:], 4, 4); o += k
+        b3 = C[o:o + 64]; o += 64
+        w4, b4 = C[o:o + 64], C[o + 64]
+        assert len(C) == o + 68
+        xo = torch.rand(8, nb * D)
+        with torch.no_grad():
+            want = c(xo).numpy()[:, 0]
+        h = np.tanh(xo.numpy() @ np.concatenate(W1s, 1).T + b1)
+        h = np.tanh(h @ W2c.T + b2)
+        h = np.tanh(h @ W3c.T + b3)
+        np.testing.assert_allclose(h @ w4 + b4, want, atol=1e-5)
