@@ -2359,6 +2359,21 @@ __device__ inline void publish_progress(int *prog, int v) {
   __hip_atomic_store(prog, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// the units kernel's per-unit LDS words (step_kernel's ushare)
+constexpr int US_STATE(int) { return 2; }
+constexpr int US_CNT(int un) { return 2 + un; }
+constexpr int US_SYNC(int un) { return 2 + 2 * un; }
+constexpr int US_PEND(int un) { return 2 + 3 * un; }
+constexpr int US_READY(int un) { return 2 + 4 * un; }
+
+// Barrier of the waves that share a counter (a unit's two waves): each wave's
+// LDS writes complete, lane 0 adds its arrival, every lane waits for `target`.
+__device__ inline void unit_arrive_wait(int *ctr, int target, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  wait_progress(ctr, target);
+}
+
 template <int NS>
 __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
                             const int *prog, float *obs_b, float *obs_r, int env0) {
@@ -2871,11 +2886,15 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   __shared__ double duct_all[UN][WAVE];
   __shared__ int prog_all[UN], qclaim_all[UN];
   __shared__ int r2_all[UN][WAVE];  // per-env max sensor reach^2 (max_range2)
-  __shared__ int ushare[2];         // UN > 1: [0] mask of quiet units, [1] shared pass counter
+  // UN > 1: [0] mask of quiet units, [1] shared pass counter (workgroup-wide
+  // barriers); with P.unit_async, per unit u: [US_STATE + u] 0 undecided / 1 quiet /
+  // 2 loud, [US_CNT + u] its pass counter, [US_SYNC + u] its two waves' barrier
+  // count, [US_PEND + u] its A* flag, [US_READY + u] its waves past phase Q
+  __shared__ int ushare[2 + 5 * UN];
   double *duct_col = duct_all[unit];
   int &prog = prog_all[unit], &qclaim = qclaim_all[unit];
   int *r2col = r2_all[unit];
-  if (UN > 1 && threadIdx.x == 0) { ushare[0] = 0; ushare[1] = 0; }  // (before phase L's barrier)
+  if (UN > 1 && (int)threadIdx.x < 2 + 5 * UN) ushare[threadIdx.x] = 0;  // (before phase L's barrier)
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
@@ -2926,22 +2945,37 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
     else
       pend = move_phase<LNW_ACT_I32, NW>(P, S, c, actions, row_kind, mask, env0, nenv, A, wid);
   }
-  // workgroup-wide: did any pair leave the move table's window (A* pass needed)?
-  const bool astar = NW > 1 ? __syncthreads_or(pend) != 0 : true;
   // quiet workgroups (lnw_quiet.inc) skip phase S; deciding it needs the final
   // moves, so wave 0 runs the A* fallback before a second barrier
   // (any workgroup size: a partial or small-epw workgroup idles its extra lanes)
   const bool qcap = ST && P.los_mode == 0 && !(P.dbg_skip & 3) && !(P.dbg_skip & 512);
+  // units kernel: the barriers below involve only this unit's two waves, so a
+  // unit whose moves finish early starts its stream without waiting for the
+  // workgroup's slowest unit (LNW_UNIT_SYNC=1: workgroup-wide barriers)
+  const bool uasync = UN > 1 && qcap && P.unit_async;
+  // did any pair leave the move table's window (A* pass needed)? (the unit's
+  // pairs, or the workgroup's)
+  bool astar = true;
+  if (uasync) {
+    if (__any(pend) && lane == 0) atomicOr(&ushare[US_PEND(UN) + unit], 1);
+    unit_arrive_wait(&ushare[US_SYNC(UN) + unit], 2, lane);
+    astar = __hip_atomic_load(&ushare[US_PEND(UN) + unit], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+  } else if (NW > 1) {
+    astar = __syncthreads_or(pend) != 0;
+  }
   if constexpr (ST && NW > 1) {
     if (qcap) {
       if (wid == 0) prof_stamp(S, 6);
       if (astar) {
         if (wid == 0) move_astar_pass(P, S, c, nenv, A);
-        __syncthreads();
+        if (uasync) unit_arrive_wait(&ushare[US_SYNC(UN) + unit], 4, lane);
+        else __syncthreads();
       }
       if (wid == 0) prof_stamp(S, 7);
       bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
       if (wid == 0) prof_stamp(S, 8);
+      if (uasync && wid == 0 && lane == 0)  // the unit decided: helpers may wait on its phase Q
+        __hip_atomic_store(&ushare[US_STATE(UN) + unit], wq ? 1 : 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef LNW_DIAG
       if (P.dbg_skip & (1 << 24)) {  // diagnostics: the quiet test again, its code now cached
         wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane] + (P.dbg_skip >> 30)));
@@ -2952,13 +2986,13 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
         if constexpr (UN > 1)
           quiet_step_units_t<NB, NR, UN>(P, S, c, lds_dyn, L, lstride, unit, lane, env, wid, duct_all,
                                          ushare, actions, obs_b, obs_r, rew_b, rew_r, done_out, cog_out,
-                                         env0, valid);
+                                         env0, valid, uasync);
         else
           quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
                                rew_r, done_out, cog_out, env0, nenv, valid);
         return;
       }
-      if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
+      if (UN > 1 && !uasync) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
     }
   }
   if (wid == 1) {
@@ -3835,6 +3869,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
   // terrain mask instead of loading LOS-table words (A/B)
   h->kp.group_march = getenv("LNW_GROUP_MARCH") != nullptr ? 1 : 0;
+  h->kp.unit_async = getenv("LNW_UNIT_SYNC") == nullptr ? 1 : 0;
   // write-through observation stores (st_obs4) while a side's output fits the
   // 32-bit buffer offsets; LNW_NO_STORE_WT keeps non-temporal stores (A/B)
   {

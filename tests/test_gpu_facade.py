@@ -101,7 +101,7 @@ def test_facade_analytics_side_channels(tmp_path, monkeypatch):
     g = Game()
     g.scenario.landing_ops = False
     g.scenario.n_red_landingship = 0
-    blue = [ShipSpec("blue", blue_type, p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
+    blue = [ShipSpec("blue", "small", p) for p in [(36, 50), (40, 52), (38, 47), (42, 44)]]
     red = [ShipSpec("red", "large", p) for p in [(58, 55), (60, 60), (62, 52), (57, 64)]]
     rng = np.random.default_rng(4)
     for ep in range(6):

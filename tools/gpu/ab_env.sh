@@ -9,7 +9,7 @@ for r in $(seq "$ROUNDS"); do
     for on in 0 1; do
       if [ "$on" = 1 ]; then export "$VAR"=1; else unset "$VAR"; fi
       timeout -k 10 120 python bench.py --no-secondary --no-cpu-baseline --steps 200 --warmup 20 $args \
-        > gpurun_out/ab.json 2>/dev/null || exit 1
+        > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -15 gpurun_out/ab.err; exit 1; }
       python -c "import json; d=json.load(open('gpurun_out/ab.json')); print('r$r', '$VAR=$on', '$args', round(d['roofline']['kernel_ms_mean']*1e3, 2), 'us')"
     done
   done
