@@ -79,6 +79,10 @@ constexpr int CH_THREADS = 256;
 // conv1 maps.
 __device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pc, int stride,
                                               bool running, float (&h)[12]) {
+  // multiply-adds fused here (the build's -ffp-contract=off is for the step
+  // kernels' bit-exactness; the policy is held to the tolerance of fp32 torch,
+  // whose conv kernels fuse them too): half the VALU work of the head
+#pragma clang fp contract(fast)
   float win[WIN];
 #pragma unroll
   for (int i = 0; i < WIN; i++) win[i] = x[i];

@@ -48,7 +48,7 @@ struct KParams {
   double det_q[2];    // detected_prob: [0] target radar==1 (0.345-0.1), [1] otherwise
   int box_lo[2], box_hi[2];
   int group_march;    // group kernel: pair LOS marched over the LDS terrain mask instead of LOS-table loads (LNW_GROUP_MARCH)
-  int unit_async;     // units kernel: phases M and Q synchronised per 64-env unit (its two waves), not workgroup-wide (LNW_UNIT_SYNC=1 restores the barriers)
+  int unit_async;     // units kernel: phases M and Q synchronised per 64-env unit (its two waves), not workgroup-wide (LNW_UNIT_ASYNC=1; off by default: 43.3 vs 42.3 us at 65 536 envs, interleaved A/B)
   int xcd_remap;      // env chunks dealt to workgroups XCD-contiguously (xcd_chunk); LNW_NO_XCD_REMAP turns it off (A/B)
   int wc[2];          // observation window cells per side: 49 (7x7), or 25 for a side of medium ships (5x5, game.py:595-610)
   int epw;            // environments per workgroup (<= EPW; fewer when E is small, to fill the CUs)

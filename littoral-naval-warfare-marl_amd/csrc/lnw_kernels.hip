@@ -2951,7 +2951,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   const bool qcap = ST && P.los_mode == 0 && !(P.dbg_skip & 3) && !(P.dbg_skip & 512);
   // units kernel: the barriers below involve only this unit's two waves, so a
   // unit whose moves finish early starts its stream without waiting for the
-  // workgroup's slowest unit (LNW_UNIT_SYNC=1: workgroup-wide barriers)
+  // workgroup's slowest unit (LNW_UNIT_ASYNC=1; measured slower, so off: the
+  // units' streams then interleave four address ranges instead of one)
   const bool uasync = UN > 1 && qcap && P.unit_async;
   // did any pair leave the move table's window (A* pass needed)? (the unit's
   // pairs, or the workgroup's)
@@ -3869,7 +3870,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
   // terrain mask instead of loading LOS-table words (A/B)
   h->kp.group_march = getenv("LNW_GROUP_MARCH") != nullptr ? 1 : 0;
-  h->kp.unit_async = getenv("LNW_UNIT_SYNC") == nullptr ? 1 : 0;
+  h->kp.unit_async = getenv("LNW_UNIT_ASYNC") != nullptr ? 1 : 0;
   // write-through observation stores (st_obs4) while a side's output fits the
   // 32-bit buffer offsets; LNW_NO_STORE_WT keeps non-temporal stores (A/B)
   {

@@ -1,8 +1,6 @@
-# round 4, iteration 5: melee aligned rows, unit-local barriers, group march, config-5 epw
 set -o pipefail
+timeout -k 10 200 python tools/policy_probe.py littoral-naval-warfare-marl_amd/lnw/liblnw.so tools/probe/actor_base.so tools/probe/actor_NOCONV.so tools/probe/actor_NOMLP.so || exit 1
 export TMPDIR=/tmp
-echo "== headline / shard: unit-local barriers (0) vs workgroup barriers (LNW_UNIT_SYNC=1)"
-bash tools/gpu/ab_env.sh LNW_UNIT_SYNC 3 "" "--global-envs 8192" || exit 6
 echo "== melee: line-aligned rows (0) vs row pieces (8192)"
 bash tools/gpu/skip_ab.sh "--spawns melee" 0 8192 0 8192 || exit 3
 for b in 0 8192; do
