@@ -337,21 +337,6 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   const int n = a.n, D = a.D;
   const long long rows = a.E * n;
   const long long r0 = (long long)blockIdx.x * CH_THREADS;
-  // observation copy for the rollout buffer: the block's rows, float4 chunks
-  if (a.obs_out) {
-    const int D4 = D >> 2;
-    const long long nr = rows - r0 < CH_THREADS ? rows - r0 : CH_THREADS;
-    const f32x4 *src = (const f32x4 *)(a.obs + r0 * D);
-    for (int q = threadIdx.x; q < nr * D4; q += CH_THREADS) {
-      const long long r = r0 + q / D4;
-      const int c4 = q - (q / D4) * D4;
-      const long long e = r / n;
-      const int i = (int)(r - e * n);
-      f32x4 v = src[q];
-      if (a.live && !a.live[e]) v = f32x4{0.f, 0.f, 0.f, 0.f};
-      *(f32x4 *)(a.obs_out + e * a.obs_env_stride + (long long)i * D + 4 * c4) = v;
-    }
-  }
   __syncthreads();
   const int lane = threadIdx.x & (WAVE - 1), g = lane >> 4, m = lane & 15;
   const long long r = r0 + threadIdx.x;
@@ -395,6 +380,26 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   } else {
 #pragma unroll
     for (int k = 0; k < NI; k++) u[k] = 0.f;
+  }
+  // ---- observation copy for the rollout buffer: the wave's 64 rows, float4
+  // chunks (coalesced; the rows are L2-warm from the conv head's reads). Here,
+  // between the VALU-bound head and the MFMA layers, rather than ahead of the
+  // head: every workgroup starts at once, so a copy there left the memory
+  // system idle during the compute and the ALUs idle during the copy.
+  if (a.obs_out) {
+    const int D4 = D >> 2;
+    const long long rw = r0 + (threadIdx.x & ~(WAVE - 1));
+    const long long nr = rows - rw < WAVE ? rows - rw : WAVE;
+    const f32x4 *src = (const f32x4 *)(a.obs + rw * D);
+    for (int q = lane; q < nr * D4; q += WAVE) {
+      const long long rr = rw + q / D4;
+      const int c4 = q - (q / D4) * D4;
+      const long long ee = rr / n;
+      const int ii = (int)(rr - ee * n);
+      f32x4 v = src[q];
+      if (a.live && !a.live[ee]) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      *(f32x4 *)(a.obs_out + ee * a.obs_env_stride + (long long)ii * D + 4 * c4) = v;
+    }
   }
   // ---- fc1 input tile: the wave's rows into the MFMA B layout ---------------
   // (over the wave's own conv1 area: its lanes are done with it, and a wave's

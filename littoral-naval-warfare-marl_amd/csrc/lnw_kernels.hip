@@ -2699,9 +2699,21 @@ __device__ inline void prof_stamp(const KState &S, int slot) {
 __device__ __forceinline__ int env_tail_core(const KParams &P, Cols &c, int lane, int nb, int A,
                                              const Neut &N, int (&ev)[8], const int (&hits)[2],
                                              int nbp, int nrp, int bsx, int bsy, int rsx, int rsy,
-                                             double *cog_p) {
+                                             double *cog_p, bool bonus_folded = false) {
   int done = 1;
   double cog = NAN;
+  // quiet steps (bonus_folded: the caller added the zero team bonus, +0.0, to
+  // every live ship's reward as it computed it): with both sides afloat and no
+  // landing ops nothing below changes a reward, so skip the per-agent passes
+  if (bonus_folded && !P.landing_ops && ev[0] != 0 && ev[1] != 0) {
+    ev[2] = ev[2] + 1;
+    if (nbp > 0 && nrp > 0) {
+      double bx = (double)bsx / nbp, by = (double)bsy / nbp, rx = (double)rsx / nrp, ry = (double)rsy / nrp;
+      cog = sqrt((bx - rx) * (bx - rx) + (by - ry) * (by - ry));
+    }
+    *cog_p = cog;
+    return done;
+  }
   // ---- tail (game.py:409-520) -------------------------------------------
   int nbl = ev[0] - N.cnt[0];
   int nrl = ev[1] - N.cnt[1];
@@ -2786,7 +2798,7 @@ __device__ __forceinline__ void env_tail(const KParams &P, const KState &S, Cols
   const long long E = P.E;
   const int nr = A - nb;
   double cog;
-  const int done = env_tail_core(P, c, lane, nb, A, N, ev, hits, nbp, nrp, bsx, bsy, rsx, rsy, &cog);
+  const int done = env_tail_core(P, c, lane, nb, A, N, ev, hits, nbp, nrp, bsx, bsy, rsx, rsy, &cog, quiet);
   const int steps_env = ev[2];
   // outputs
   // float32 values by default; float64 (the reference's Python floats) when
@@ -3521,6 +3533,7 @@ struct lnw_handle {
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
   bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
+  bool force_group = false;  // LNW_FORCE_GROUP (A/B): the group kernel for templated team sizes too
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
@@ -3863,6 +3876,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->force_generic = getenv("LNW_FORCE_GENERIC") != nullptr;
   // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
+  h->force_group = getenv("LNW_FORCE_GROUP") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
   // LNW_NO_XCD_REMAP: workgroup b steps env chunk b (A/B tests of xcd_chunk)
@@ -4157,7 +4171,8 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   hipStream_t st = (hipStream_t)stream;
   // (medium ships: 5x5 windows and shorter rows, the runtime-size kernels only)
   bool generic = h->force_generic;
-  const bool templated = k.los_mode != 2 && !generic && !h->has_medium && h->nb == h->nr && h->nb >= 2 && h->nb <= 4;
+  const bool templated = k.los_mode != 2 && !generic && !h->has_medium && h->nb == h->nr && h->nb >= 2 && h->nb <= 4 &&
+                         !(h->force_group && h->group_fits);
   const bool use_group = k.los_mode != 2 && !templated && !generic && !h->no_group && h->group_fits;
   // 4v4 at 64 envs per workgroup in LOS-table mode, whole units (the headline):
   // the units kernel (LNW_NO_UNITS keeps one unit per workgroup)
