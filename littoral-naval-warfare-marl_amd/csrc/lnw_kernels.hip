@@ -1979,30 +1979,15 @@ __device__ __forceinline__ void write_obs(const KParams &P, const KState &S, Col
 // own ship s < kl ? s : s + 1 (combatant.py:190-212), and the row leaves as
 // D/4 ds_write_b128. Combatant rows: window[49] | tail; LandingShip rows:
 // window[25] | tail | zeros (the LS window record is zero past 25 floats).
+// The row from its inputs (the own ship's cell, type, alive flag, radar,
+// missiles, target count, the env's ducting; teammate slot s's cell, radar,
+// missiles, type, alive flag) and the ship's window record in v / w48.
 template <int NS>
-__device__ inline void row_regs_t(const Cols &c, const double *duct_col, int el, int k, int own0,
-                                  const f32x4 (&v)[12], float w48, float *row, const float *xg) {
+__device__ __forceinline__ void row_build_t(uint32_t p, int tk, int alive, int rad, int mis, uint32_t tcn, double du,
+                                   const uint32_t (&tq)[NS - 1], const int (&tr)[NS - 1], const int (&tm)[NS - 1],
+                                   const int (&tt)[NS - 1], const int (&ta)[NS - 1], const f32x4 (&v)[12],
+                                   float w48, float *row, const float *xg) {
   constexpr int D = 4 * NS + 52, T = 4 * NS + 3;
-  const int kl = k - own0;
-  const uint32_t p = c.pos_cur[k * PAD + el];
-  const int tk = c.type[k * PADB + el];
-  const int alive = c.alive0[k * PADB + el];
-  const int rad = c.radar_cur[k * PAD + el];
-  const int mis = c.miss_cur[k * PADB + el];
-  const uint32_t tcn = c.tcnt[k * PAD + el];
-  const double du = duct_col[el];
-  uint32_t tq[NS - 1];
-  int tr[NS - 1], tm[NS - 1], tt[NS - 1], ta[NS - 1];
-#pragma unroll
-  for (int s = 0; s < NS - 1; s++) {
-    const bool nw = s < kl;  // own ships that acted before k show their new state
-    const int i = own0 + (nw ? s : s + 1);
-    tq[s] = (nw ? c.pos_cur : c.pos_old)[i * PAD + el];
-    tr[s] = (nw ? c.radar_cur : c.radar_old)[i * PAD + el];
-    tm[s] = (nw ? c.miss_cur : c.miss_old)[i * PADB + el];
-    tt[s] = c.type[i * PADB + el];
-    ta[s] = c.alive0[i * PADB + el];
-  }
   float t[T];
   t[0] = xg[pos_x(p)];
   t[1] = xg[pos_y(p)];
@@ -2035,6 +2020,27 @@ __device__ inline void row_regs_t(const Cols &c, const double *duct_col, int el,
     }
     r4[q] = o;
   }
+}
+
+template <int NS>
+__device__ inline void row_regs_t(const Cols &c, const double *duct_col, int el, int k, int own0,
+                                  const f32x4 (&v)[12], float w48, float *row, const float *xg) {
+  const int kl = k - own0;
+  uint32_t tq[NS - 1];
+  int tr[NS - 1], tm[NS - 1], tt[NS - 1], ta[NS - 1];
+#pragma unroll
+  for (int s = 0; s < NS - 1; s++) {
+    const bool nw = s < kl;  // own ships that acted before k show their new state
+    const int i = own0 + (nw ? s : s + 1);
+    tq[s] = (nw ? c.pos_cur : c.pos_old)[i * PAD + el];
+    tr[s] = (nw ? c.radar_cur : c.radar_old)[i * PAD + el];
+    tm[s] = (nw ? c.miss_cur : c.miss_old)[i * PADB + el];
+    tt[s] = c.type[i * PADB + el];
+    ta[s] = c.alive0[i * PADB + el];
+  }
+  row_build_t<NS>(c.pos_cur[k * PAD + el], c.type[k * PADB + el], c.alive0[k * PADB + el],
+                  c.radar_cur[k * PAD + el], c.miss_cur[k * PADB + el], c.tcnt[k * PAD + el], duct_col[el], tq,
+                  tr, tm, tt, ta, v, w48, row, xg);
 }
 
 template <int NS, int NPASS4, bool NT = true>
