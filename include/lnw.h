@@ -160,6 +160,10 @@ int lnw_set_rng(lnw_handle *h, int32_t mode, uint64_t seed, const double *tape_d
 int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn,
               const int32_t *pos_dev, void *stream);
 
+/* obs_blue_dev and obs_red_dev both NULL: no observation rows are written
+ * (the MAPPO rollout discards step()'s observations, ppo.py:577, and observes
+ * afresh); every other effect of the step is unchanged. One NULL alone is
+ * LNW_EINVAL. */
 int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
              float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
              int32_t *done_dev, float *cog_dev, void *stream);
@@ -169,6 +173,12 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
  * in list order. Side effects as the reference (target lists, RNG draws). */
 int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_red_dev,
                 void *stream);
+/* lnw_observe with the rows of env e at obs + e * stride (floats; 0 = the
+ * packed n * D; else a multiple of 4, at least n * D) and NULL for a side whose
+ * rows nobody reads (its get_obs calls and their side effects still run):
+ * the MAPPO rollout observes straight into its buffer (ppo.py:497-575). */
+int lnw_observe_ex(lnw_handle *h, int32_t agent, float *obs_blue_dev, int64_t blue_env_stride,
+                   float *obs_red_dev, int64_t red_env_stride, void *stream);
 
 /* ---- state access (tests, facade, checkpoint) --------------------------- */
 #define LNW_F_POS 0        /* [A][E] u32: x | y<<16                          */
@@ -368,6 +378,10 @@ typedef struct lnw_policy_args {
   int32_t kinds_f32_all_alive; /* 1: LNW_KIND_F32 rows when every ship is alive, else F64 */
   uint8_t *f32_out;            /* NULL, or env e at f32_out[e * f32_env_stride]: the rows are F32 */
   int64_t f32_env_stride;
+  int64_t obs_in_env_stride;   /* floats between envs' rows in obs (0: n * D). obs_out == obs with
+                                  obs_env_stride == this stride: the rows already sit in the rollout
+                                  buffer (lnw_observe_ex wrote them there), and only the rows of
+                                  envs whose episode ended (live == 0) are zeroed in place */
 } lnw_policy_args;
 int lnw_policy_act(const lnw_policy_args *args, void *stream);
 

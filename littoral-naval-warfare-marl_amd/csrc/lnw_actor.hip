@@ -337,6 +337,7 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   const int n = a.n, D = a.D;
   const long long rows = a.E * n;
   const long long r0 = (long long)blockIdx.x * CH_THREADS;
+  const long long istride = a.obs_in_env_stride ? a.obs_in_env_stride : (long long)n * D;
   __syncthreads();
   const int lane = threadIdx.x & (WAVE - 1), g = lane >> 4, m = lane & 15;
   const long long r = r0 + threadIdx.x;
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   // ---- conv head + LayerNorm, one row per lane -------------------------------
   float u[NI];
   if (valid) {
-    const float *x = a.obs + r * D;
+    const float *x = a.obs + e * istride + (long long)i * D;
     float h[12];
 #ifdef LNW_PROBE_NOCONV  // timing probes only (tools/policy_probe.py): no conv head
     for (int k = 0; k < 12; k++) h[k] = x[k];
@@ -386,18 +387,21 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   // between the VALU-bound head and the MFMA layers, rather than ahead of the
   // head: every workgroup starts at once, so a copy there left the memory
   // system idle during the compute and the ALUs idle during the copy.
-  if (a.obs_out) {
+  // (in place: lnw_observe_ex wrote the rows into the rollout buffer itself;
+  // only the rows of envs whose episode ended are zeroed)
+  const bool in_place = a.obs_out == a.obs && a.obs_env_stride == istride;
+  if (a.obs_out && (!in_place || a.live)) {
     const int D4 = D >> 2;
     const long long rw = r0 + (threadIdx.x & ~(WAVE - 1));
     const long long nr = rows - rw < WAVE ? rows - rw : WAVE;
-    const f32x4 *src = (const f32x4 *)(a.obs + rw * D);
     for (int q = lane; q < nr * D4; q += WAVE) {
       const long long rr = rw + q / D4;
       const int c4 = q - (q / D4) * D4;
       const long long ee = rr / n;
       const int ii = (int)(rr - ee * n);
-      f32x4 v = src[q];
-      if (a.live && !a.live[ee]) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool dead = a.live && !a.live[ee];
+      if (in_place && !dead) continue;
+      f32x4 v = dead ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4 *)(a.obs + ee * istride + (long long)ii * D + 4 * c4);
       *(f32x4 *)(a.obs_out + ee * a.obs_env_stride + (long long)ii * D + 4 * c4) = v;
     }
   }
@@ -685,6 +689,9 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   if (!a.forced && a.T <= 0) return LNW_EINVAL;
   if (a.script && (!a.full || a.script_own0 < 0 || a.script_own0 + a.script_cnt > a.A)) return LNW_EINVAL;
   if ((a.kinds_f32_all_alive || a.f32_out) && !a.kinds) return LNW_EINVAL;
+  if (a.obs_in_env_stride < 0 || (a.obs_in_env_stride && (a.obs_in_env_stride < (int64_t)a.n * a.D ||
+                                                          (a.obs_in_env_stride & 3))))
+    return LNW_EINVAL;
   // 16-B aligned rows for the vector copies and stores
   if (((uintptr_t)a.obs & 15) || (a.obs_out && (((uintptr_t)a.obs_out & 15) || (a.obs_env_stride & 3))) ||
       ((a.act_out || a.logp_out) && (a.act_env_stride & 3)) || (a.act_out && ((uintptr_t)a.act_out & 15)) ||

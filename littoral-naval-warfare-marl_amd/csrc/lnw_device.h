@@ -48,12 +48,13 @@ struct KParams {
   double det_q[2];    // detected_prob: [0] target radar==1 (0.345-0.1), [1] otherwise
   int box_lo[2], box_hi[2];
   int group_march;    // group kernel: pair LOS marched over the LDS terrain mask instead of LOS-table loads (LNW_GROUP_MARCH)
-  int unit_async;     // units kernel: phases M and Q synchronised per 64-env unit (its two waves), not workgroup-wide (LNW_UNIT_ASYNC=1; off by default: 43.3 vs 42.3 us at 65 536 envs, interleaved A/B)
   int xcd_remap;      // env chunks dealt to workgroups XCD-contiguously (xcd_chunk); LNW_NO_XCD_REMAP turns it off (A/B)
   int wc[2];          // observation window cells per side: 49 (7x7), or 25 for a side of medium ships (5x5, game.py:595-610)
   int epw;            // environments per workgroup (<= EPW; fewer when E is small, to fill the CUs)
   int store_wt;       // observation stream stored write-through (sc1): no dirty lines left in L2 at the launch end
   int atan_odd;       // the host's bearing table is odd in dy (degrees(atan2(-dy, dx)) == -degrees(atan2(dy, dx))): the group kernel stages its dy >= 0 half
+  int no_obs;         // lnw_step without observation outputs (both pointers NULL)
+  long long obs_stride[2];  // lnw_observe_ex: floats between envs' rows per side (0: packed)
   int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table, bit13 4-ship phase-S rows stored row by row instead of line-aligned
 };
 
@@ -391,7 +392,7 @@ __device__ __forceinline__ int xcd_chunk(const KParams &P, int b, int nwg) {
   return (b & 7) * (nwg >> 3) + (b >> 3);
 }
 // observation row length of a side: 4 n + window + 3 (game.py:609-610)
-__device__ inline int side_D(const KParams &P, int side) {
+__host__ __device__ inline int side_D(const KParams &P, int side) {
   return 4 * (side ? P.nr : P.nb) + P.wc[side ? 1 : 0] + 3;
 }
 __device__ inline int mast_cls(int t) { return t == T_SMALL ? 0 : 1; }

@@ -1920,13 +1920,23 @@ __device__ __forceinline__ void build_row(const KParams &P, const KState &S, con
 // a side of medium ships) with each lane moving 4 consecutive floats:
 // ds_read_b128 from the staged row, dwordx4 store (1 KiB per wave store
 // instruction).
-__device__ inline void copy_side(const float *stage, float *out, int ns, int D, int ne, long long genv0) {
+// stride: floats between envs' rows in out (0: packed, ns * D)
+__device__ inline void copy_side(const float *stage, float *out, int ns, int D, int ne, long long genv0,
+                                 long long stride = 0) {
   if (!out) return;
   const int lane = threadIdx.x & (WAVE - 1);
   const int S4 = stage_stride(ns) >> 2;
   const int D4 = D >> 2;
   const int n4 = ne * ns * D4;
   const f32x4 *st4 = (const f32x4 *)stage;
+  if (stride && stride != (long long)ns * D) {
+    const int per = ns * D4;  // float4 chunks per env
+    for (int i = lane; i < n4; i += WAVE) {
+      const int e = i / per, q = i - e * per, r = e * ns + q / D4;
+      ((f32x4 *)(out + (genv0 + e) * stride))[q] = st4[r * S4 + (q - (q / D4) * D4)];
+    }
+    return;
+  }
   f32x4 *base = (f32x4 *)(out + (size_t)genv0 * ns * D);
   int r = lane / D4, c4 = lane - r * D4;
   for (int i = lane; i < n4; i += WAVE) {
@@ -1963,8 +1973,8 @@ __device__ __forceinline__ void write_obs(const KParams &P, const KState &S, Col
       build_row(P, S, c, duct_col, g0 + my_e, my_k, row, xg, only_observed);
     wave_lds_sync();
     if (!(P.dbg_skip & 16)) {
-      copy_side(stage_b, obs_b, nb, side_D(P, 0), ne, env0 + g0);
-      copy_side(stage_r, obs_r, nr, side_D(P, 1), ne, env0 + g0);
+      copy_side(stage_b, obs_b, nb, side_D(P, 0), ne, env0 + g0, P.obs_stride[0]);
+      copy_side(stage_r, obs_r, nr, side_D(P, 1), ne, env0 + g0, P.obs_stride[1]);
     }
     wave_lds_sync();
   }
@@ -2365,20 +2375,6 @@ __device__ inline void publish_progress(int *prog, int v) {
   __hip_atomic_store(prog, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// the units kernel's per-unit LDS words (step_kernel's ushare)
-constexpr int US_STATE(int) { return 2; }
-constexpr int US_CNT(int un) { return 2 + un; }
-constexpr int US_SYNC(int un) { return 2 + 2 * un; }
-constexpr int US_PEND(int un) { return 2 + 3 * un; }
-constexpr int US_READY(int un) { return 2 + 4 * un; }
-
-// Barrier of the waves that share a counter (a unit's two waves): each wave's
-// LDS writes complete, lane 0 adds its arrival, every lane waits for `target`.
-__device__ inline void unit_arrive_wait(int *ctr, int target, int lane) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  wait_progress(ctr, target);
-}
 
 template <int NS>
 __device__ __forceinline__ void emit_wave_t(const KParams &P, const KState &S, const Cols &c, const double *duct_col,
@@ -2904,19 +2900,15 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   __shared__ double duct_all[UN][WAVE];
   __shared__ int prog_all[UN], qclaim_all[UN];
   __shared__ int r2_all[UN][WAVE];  // per-env max sensor reach^2 (max_range2)
-  // UN > 1: [0] mask of quiet units, [1] shared pass counter (workgroup-wide
-  // barriers); with P.unit_async, per unit u: [US_STATE + u] 0 undecided / 1 quiet /
-  // 2 loud, [US_CNT + u] its pass counter, [US_SYNC + u] its two waves' barrier
-  // count, [US_PEND + u] its A* flag, [US_READY + u] its waves past phase Q
-  __shared__ int ushare[2 + 5 * UN];
+  __shared__ int ushare[2];         // UN > 1: [0] mask of quiet units, [1] shared pass counter
   double *duct_col = duct_all[unit];
   int &prog = prog_all[unit], &qclaim = qclaim_all[unit];
   int *r2col = r2_all[unit];
-  if (UN > 1 && (int)threadIdx.x < 2 + 5 * UN) ushare[threadIdx.x] = 0;  // (before phase L's barrier)
+  if (UN > 1 && threadIdx.x == 0) { ushare[0] = 0; ushare[1] = 0; }  // (before phase L's barrier)
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
-  const bool emit = ST && P.los_mode != 1 && nenv == WAVE && !(P.dbg_skip & 3);
+  const bool emit = ST && P.los_mode != 1 && nenv == WAVE && !(P.dbg_skip & 3) && !P.no_obs;
   // two-wave workgroups share phases L and M (agents / pair passes split);
   // after M wave 1 turns to emission and wave 0 runs S
   constexpr int NW = ST && EPW == WAVE ? 2 : 1;
@@ -2967,34 +2959,20 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   // moves, so wave 0 runs the A* fallback before a second barrier
   // (any workgroup size: a partial or small-epw workgroup idles its extra lanes)
   const bool qcap = ST && P.los_mode == 0 && !(P.dbg_skip & 3) && !(P.dbg_skip & 512);
-  // units kernel: the barriers below involve only this unit's two waves, so a
-  // unit whose moves finish early starts its stream without waiting for the
-  // workgroup's slowest unit (LNW_UNIT_ASYNC=1; measured slower, so off: the
-  // units' streams then interleave four address ranges instead of one)
-  const bool uasync = UN > 1 && qcap && P.unit_async;
-  // did any pair leave the move table's window (A* pass needed)? (the unit's
-  // pairs, or the workgroup's)
-  bool astar = true;
-  if (uasync) {
-    if (__any(pend) && lane == 0) atomicOr(&ushare[US_PEND(UN) + unit], 1);
-    unit_arrive_wait(&ushare[US_SYNC(UN) + unit], 2, lane);
-    astar = __hip_atomic_load(&ushare[US_PEND(UN) + unit], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-  } else if (NW > 1) {
-    astar = __syncthreads_or(pend) != 0;
-  }
+  // workgroup-wide: did any pair leave the move table's window (A* pass needed)?
+  // (round 4 measured unit-local barriers here and after phase Q instead,
+  // each unit streaming as soon as its own moves were final: 43.3 vs 42.3 us)
+  const bool astar = NW > 1 ? __syncthreads_or(pend) != 0 : true;
   if constexpr (ST && NW > 1) {
     if (qcap) {
       if (wid == 0) prof_stamp(S, 6);
       if (astar) {
         if (wid == 0) move_astar_pass(P, S, c, nenv, A);
-        if (uasync) unit_arrive_wait(&ushare[US_SYNC(UN) + unit], 4, lane);
-        else __syncthreads();
+        __syncthreads();
       }
       if (wid == 0) prof_stamp(S, 7);
       bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
       if (wid == 0) prof_stamp(S, 8);
-      if (uasync && wid == 0 && lane == 0)  // the unit decided: helpers may wait on its phase Q
-        __hip_atomic_store(&ushare[US_STATE(UN) + unit], wq ? 1 : 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef LNW_DIAG
       if (P.dbg_skip & (1 << 24)) {  // diagnostics: the quiet test again, its code now cached
         wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane] + (P.dbg_skip >> 30)));
@@ -3005,13 +2983,13 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
         if constexpr (UN > 1)
           quiet_step_units_t<NB, NR, UN>(P, S, c, lds_dyn, L, lstride, unit, lane, env, wid, duct_all,
                                          ushare, actions, obs_b, obs_r, rew_b, rew_r, done_out, cog_out,
-                                         env0, valid, uasync);
+                                         env0, valid);
         else
           quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
                                rew_r, done_out, cog_out, env0, nenv, valid);
         return;
       }
-      if (UN > 1 && !uasync) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
+      if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
     }
   }
   if (wid == 1) {
@@ -3161,7 +3139,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
       for (int q = 0; q < 4; q++) prof_put(S, 16 + q, tp[q]);
   }
   prof_stamp(S, 3);
-  if ((P.dbg_skip & 1) || emit) return;
+  if ((P.dbg_skip & 1) || emit || P.no_obs) return;
   __syncthreads();
   // ---- phase O: observations ---------------------------------------------
   if constexpr (ST) write_obs_t<NB, NR>(P, S, c, duct_col, obs_b, obs_r, env0, nenv);
@@ -3890,7 +3868,6 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
   // terrain mask instead of loading LOS-table words (A/B)
   h->kp.group_march = getenv("LNW_GROUP_MARCH") != nullptr ? 1 : 0;
-  h->kp.unit_async = getenv("LNW_UNIT_ASYNC") != nullptr ? 1 : 0;
   // write-through observation stores (st_obs4) while a side's output fits the
   // 32-bit buffer offsets; LNW_NO_STORE_WT keeps non-temporal stores (A/B)
   {
@@ -4167,8 +4144,11 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
     return fail(LNW_EINVAL, "integer actions go with DISCRETE mode only");
   if (action_dtype == LNW_ACT_F32 && h->params.discrete)
     return fail(LNW_EINVAL, "DISCRETE mode takes int32 (ndarray) or float64 (list rows) actions");
+  if ((obs_blue_dev == nullptr) != (obs_red_dev == nullptr))
+    return fail(LNW_EINVAL, "observation outputs: both or neither");
   KParams k = h->kp;
   k.act_dtype = action_dtype;
+  k.no_obs = obs_blue_dev == nullptr ? 1 : 0;
   k.dbg_skip = h->dbg_skip;
   k.store_wt = h->store_wt;
   KState s = make_state(h);
@@ -4237,17 +4217,30 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
 }
 
 int lnw_observe(lnw_handle *h, int32_t agent, float *obs_blue_dev, float *obs_red_dev, void *stream) {
+  return lnw_observe_ex(h, agent, obs_blue_dev, 0, obs_red_dev, 0, stream);
+}
+
+int lnw_observe_ex(lnw_handle *h, int32_t agent, float *obs_blue_dev, int64_t blue_env_stride,
+                   float *obs_red_dev, int64_t red_env_stride, void *stream) {
   if (!h) return fail(LNW_EINVAL, "null handle");
   if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
   if (agent >= h->A || agent < LNW_OBS_RED) return fail(LNW_EINVAL, "bad agent selector");
+  const int64_t row_b = (int64_t)h->nb * side_D(h->kp, 0), row_r = (int64_t)h->nr * side_D(h->kp, 1);
+  if (blue_env_stride < 0 || red_env_stride < 0 || (blue_env_stride && (blue_env_stride < row_b || blue_env_stride % 4)) ||
+      (red_env_stride && (red_env_stride < row_r || red_env_stride % 4)))
+    return fail(LNW_EINVAL, "env stride: 0, or a multiple of 4 floats of at least the side's n * D");
+  if (((uintptr_t)obs_blue_dev | (uintptr_t)obs_red_dev) & 15) return fail(LNW_EINVAL, "rows must be 16-B aligned");
   KState s = make_state(h);
   size_t lds = step_lds_bytes(h);
   dim3 grid((h->E + h->kp.epw - 1) / h->kp.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
   const bool tmpl = !h->force_generic && !h->has_medium && h->params.los_mode != 2 && h->nb == h->nr;
   const bool cw = h->contact;
+  KParams k = h->kp;
+  k.obs_stride[0] = blue_env_stride;
+  k.obs_stride[1] = red_env_stride;
 #define LNW_OBS(NB_, CW_) \
-  observe_kernel<NB_, NB_, CW_><<<grid, block, lds, st>>>(h->kp, s, agent, obs_blue_dev, obs_red_dev)
+  observe_kernel<NB_, NB_, CW_><<<grid, block, lds, st>>>(k, s, agent, obs_blue_dev, obs_red_dev)
   if (tmpl && h->nb == 4) { if (cw) LNW_OBS(4, true); else LNW_OBS(4, false); }
   else if (tmpl && h->nb == 3) { if (cw) LNW_OBS(3, true); else LNW_OBS(3, false); }
   else if (tmpl && h->nb == 2) { if (cw) LNW_OBS(2, true); else LNW_OBS(2, false); }

@@ -23,7 +23,7 @@ LNW_ERRF_ZERODIV, LNW_ERRF_NAN_ROUND, LNW_ERRF_TAPE, LNW_ERRF_MISSILES = 1, 2, 4
 # exported symbols (must match include/lnw.h)
 SYMBOLS = [
     "lnw_abi_version", "lnw_last_error", "lnw_create", "lnw_destroy", "lnw_load_terrain",
-    "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_state_field", "lnw_tlist_cap",
+    "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_observe_ex", "lnw_state_field", "lnw_tlist_cap",
     "lnw_set_epw", "lnw_set_variant", "lnw_set_reward_dtype",
     "lnw_set_counters",
     "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
@@ -70,7 +70,8 @@ class PolicyArgs(C.Structure):  # include/lnw.h: lnw_policy_args
                 ("full", C.c_void_p), ("script", C.c_void_p),
                 ("script_n", C.c_int32), ("script_steps", C.c_int32), ("script_own0", C.c_int32),
                 ("script_cnt", C.c_int32), ("kinds", C.c_void_p), ("kinds_f32_all_alive", C.c_int32),
-                ("f32_out", C.c_void_p), ("f32_env_stride", C.c_int64)]
+                ("f32_out", C.c_void_p), ("f32_env_stride", C.c_int64),
+                ("obs_in_env_stride", C.c_int64)]
 
 
 class RolloutPostArgs(C.Structure):  # include/lnw.h: lnw_rollout_post_args
@@ -110,6 +111,7 @@ def load(path=None):
         "lnw_reset": ([P, P, C.POINTER(Spawn), P, P], C.c_int),
         "lnw_step": ([P, P, I32, P, P, P, P, P, P, P, P], C.c_int),
         "lnw_observe": ([P, I32, P, P, P], C.c_int),
+        "lnw_observe_ex": ([P, I32, P, C.c_int64, P, C.c_int64, P], C.c_int),
         "lnw_state_field": ([P, I32, C.POINTER(P), C.POINTER(I64)], C.c_int),
         "lnw_tlist_cap": ([P], C.c_int),
         "lnw_set_epw": ([P, I32], C.c_int),

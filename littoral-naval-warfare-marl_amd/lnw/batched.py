@@ -182,10 +182,12 @@ class BatchedGame:
             torch.cuda.current_stream(self.device).synchronize()
 
     # --------------------------------------------------------------- step
-    def step(self, actions, row_kind=None):
+    def step(self, actions, row_kind=None, obs=True):
         """Game.step for all envs. actions: [E, A, 4] float32 / float64 tensor
         (continuous) or int32 (discrete). Mutated in place where the reference
-        mutates its action rows (game.py:379). Returns the output tensors."""
+        mutates its action rows (game.py:379). Returns the output tensors.
+        obs=False: no observation rows are written (obs_blue / obs_red keep
+        their contents; a caller that observes afresh, as ppo.py does)."""
         a = actions
         if a.shape != self._ashape or not a.is_cuda or not a.is_contiguous():
             raise ValueError(f"actions must be a contiguous cuda tensor of shape {tuple(self._ashape)}")
@@ -196,6 +198,8 @@ class BatchedGame:
         if row_kind is not None:
             rk = _ptr(torch.as_tensor(row_kind, dtype=torch.uint8, device=self.device).contiguous())
         ob, orr, rb, rr, dn, cg = self._outp
+        if not obs:
+            ob = orr = None
         check(self.L.lnw_step(self.h, a.data_ptr(), dt, rk, ob, orr, rb, rr, dn, cg,
                               torch.cuda.current_stream(self.device).cuda_stream))
         return self._outd
@@ -279,6 +283,13 @@ class BatchedGame:
         check(self.L.lnw_observe(self.h, int(agent), _ptr(self.obs_blue), _ptr(self.obs_red),
                                  self._stream()))
         return self.obs_blue, self.obs_red
+
+    def observe_into(self, agent, blue_ptr, blue_env_stride=0, red_ptr=None, red_env_stride=0):
+        """observe() with the rows written to caller memory (device pointers;
+        env e's rows at ptr + e * stride floats, 0 = packed) or nowhere (None:
+        the side's get_obs side effects still happen) — lnw_observe_ex."""
+        check(self.L.lnw_observe_ex(self.h, int(agent), blue_ptr, int(blue_env_stride), red_ptr,
+                                    int(red_env_stride), self._stream()))
 
     # -------------------------------------------------------------- state
     def _field(self, f):

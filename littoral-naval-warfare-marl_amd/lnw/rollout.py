@@ -428,13 +428,22 @@ class Rollout:
         f4, f8 = 4, 8
         table = self.table.contiguous() if self.table is not None else None
         rew_f64 = int(g.rew_blue.dtype == torch.float64)
+        # fresh observations with no per-step callback: the blue rows go straight
+        # into the rollout buffer (lnw_observe_ex; the policy zeroes ended envs'
+        # rows in place), red's only where a red actor reads them, and the step
+        # writes none (ppo.py:577 discards them). g.obs_blue is not updated then.
+        direct = self.observe == "fresh" and on_step is None
         if self.observe == "step":
             g.observe(-1)
         for t in range(T):
-            if self.observe == "fresh":
+            row_t = P(obs) + t * nb * Db * f4  # the rollout buffer's rows of step t
+            if direct:
+                g.observe_into(-1, row_t, T * nb * Db, P(g.obs_red) if red_actor_rows else None, 0)
+            elif self.observe == "fresh":
                 g.observe(-1)
             pa = PolicyArgs()
-            pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = P(g.obs_blue), E, nb, Db, 0, A
+            pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = (row_t if direct else P(g.obs_blue)), E, nb, Db, 0, A
+            pa.obs_in_env_stride = T * nb * Db if direct else 0
             pa.params, pa.bn_running = P(ap), int(self.bn == "running")
             if fa is not None:
                 pa.forced, pa.forced_act, pa.fa_env_stride = 1, P(fa) + t * A * 4 * f4, T * A * 4
@@ -443,7 +452,7 @@ class Rollout:
             pa.row_base = g.env_id_base * nb
             pa.alive = alive_p
             pa.live = P(live) if self.stop_at_done else None
-            pa.obs_out, pa.obs_env_stride = P(obs) + t * nb * Db * f4, T * nb * Db
+            pa.obs_out, pa.obs_env_stride = row_t, T * nb * Db
             pa.act_out, pa.logp_out = P(acts) + t * nb * 4 * f4, P(logp) + t * nb * 4 * f4
             pa.act_env_stride = T * nb * 4
             pa.full = P(full)
@@ -462,7 +471,7 @@ class Rollout:
                 ra.seed, ra.call_dev, ra.T, ra.t, ra.which = seed, P(self._call), T, t, 2
                 ra.row_base, ra.alive, ra.full = g.env_id_base * nr, alive_p, P(full)
                 _abi.check(L.lnw_policy_act(C.byref(ra), stream))
-            out = g.step(full, kinds)
+            out = g.step(full, kinds, obs=not direct)
             pp = RolloutPostArgs()
             pp.obs, pp.obs_env_stride, pp.E, pp.n, pp.D = pa.obs_out, T * nb * Db, E, nb, Db
             if cp is not None:
