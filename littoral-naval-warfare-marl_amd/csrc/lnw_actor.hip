@@ -292,6 +292,68 @@ __device__ __forceinline__ void mfma_layer(const f32x4v *__restrict__ F, const f
   }
 }
 
+// The same layers on the bf16 matrix cores at f32 accuracy (lnw_policy_act):
+// v_mfma_f32_16x16x32_bf16, lane l holding A[l & 15][k = 8 (l >> 4) + j] and
+// B[k][l & 15], j = 0..7. Element j of a k-pair p is neuron 32 p + 16 (j / 4) +
+// 4 (l >> 4) + j % 4, so the B operand of pair p is just the two f32 quads
+// (2p, 2p + 1) of mfma_layer's layout: the chaining stays register-only. Each
+// f32 value is split exactly into three bfloat16 terms (x = x0 + x1 + x2, each
+// rounded to nearest: 8 + 8 + 8 bits), the weights on the host
+// (BatchedActor.packed_policy: planes hi, mid, lo), the activations here; of
+// the nine partial products the six above 2^-24 relative are summed (small
+// ones first), so a product is exact to about 3 ulp of f32 and the sums match
+// the f32 MFMA's within a few ulp, at 6 x 16 cycles per 32 k instead of the
+// f32 form's 8 x 32.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const f32x4v &a, const f32x4v &b, bf16x8 &x0, bf16x8 &x1, bf16x8 &x2) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const float x = j < 4 ? a[j] : b[j - 4];
+    const __bf16 h = (__bf16)x;
+    const float r = x - (float)h;
+    const __bf16 m = (__bf16)r;
+    x0[j] = h;
+    x1[j] = m;
+    x2[j] = (__bf16)(r - (float)m);
+  }
+}
+
+__device__ __forceinline__ f32x4v mfma32(const bf16x8 &a, const bf16x8 &b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc[rt][nt] += W (planes F: hi | mid | lo, each bf16x8 [nt][p][lane]) x X
+template <int NTO, int Q>
+__device__ __forceinline__ void mfma_layer3(const bf16x8 *__restrict__ F, const f32x4v (&xb)[4][Q],
+                                            f32x4v (&acc)[4][NTO], int lane) {
+  static_assert(Q % 2 == 0, "k in pairs of quads");
+  constexpr int QP = Q / 2, PL = NTO * QP * WAVE;  // plane stride (bf16x8)
+#pragma unroll
+  for (int p = 0; p < QP; p++) {
+    bf16x8 b0[4], b1[4], b2[4];
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) split3(xb[rt][2 * p], xb[rt][2 * p + 1], b0[rt], b1[rt], b2[rt]);
+#pragma unroll
+    for (int nt = 0; nt < NTO; nt++) {
+      const int i = (nt * QP + p) * WAVE + lane;
+      const bf16x8 w0 = F[i], w1 = F[PL + i], w2 = F[2 * PL + i];
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) acc[rt][nt] = mfma32(w2, b0[rt], acc[rt][nt]);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) acc[rt][nt] = mfma32(w1, b1[rt], acc[rt][nt]);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) acc[rt][nt] = mfma32(w0, b2[rt], acc[rt][nt]);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) acc[rt][nt] = mfma32(w1, b0[rt], acc[rt][nt]);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) acc[rt][nt] = mfma32(w0, b1[rt], acc[rt][nt]);
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) acc[rt][nt] = mfma32(w0, b0[rt], acc[rt][nt]);
+    }
+  }
+}
+
 template <int NTO>
 __device__ __forceinline__ void bias_init(const float *__restrict__ b, f32x4v (&acc)[4][NTO], int g) {
 #pragma unroll
@@ -423,24 +485,26 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   float mean[NOUT], lsd[NOUT];
   for (int v = 0; v < NOUT; v++) { mean[v] = xb[0][0][v]; lsd[v] = 0.f; }
 #else
-  const f32x4v *Fw = (const f32x4v *)(a.params + pa.off_w1);
+  // weights: three bf16 planes per layer (mfma_layer3), layers in order
+  const bf16x8 *Fw = (const bf16x8 *)(a.params + pa.off_w1);
+  constexpr int O2 = 3 * 4 * (Q1 / 2) * WAVE, O3 = O2 + 3 * 4 * 2 * WAVE, OH = O3 + 3 * 2 * 2 * WAVE;
   const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
   f32x4v h1[4][4];
   bias_init<4>(bias, h1, g);
-  mfma_layer<4, Q1>(Fw, xb, h1, lane);
+  mfma_layer3<4, Q1>(Fw, xb, h1, lane);
   tanh_all<4>(h1);
   f32x4v h2[4][4];
   bias_init<4>(bias + 64, h2, g);
-  mfma_layer<4, 4>(Fw + 4 * Q1 * WAVE, h1, h2, lane);
+  mfma_layer3<4, 4>(Fw + O2, h1, h2, lane);
   tanh_all<4>(h2);
   f32x4v h3[4][2];
   bias_init<2>(bias + 128, h3, g);
-  mfma_layer<2, 4>(Fw + (4 * Q1 + 16) * WAVE, h2, h3, lane);
+  mfma_layer3<2, 4>(Fw + O3, h2, h3, lane);
   tanh_all<2>(h3);
   f32x4v hh[4][1];
 #pragma unroll
   for (int rt = 0; rt < 4; rt++) hh[rt][0] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  mfma_layer<1, 2>(Fw + (4 * Q1 + 24) * WAVE, h3, hh, lane);
+  mfma_layer3<1, 2>(Fw + OH, h3, hh, lane);
   // head outputs of row 16 rt + m sit in lane m (normal head, n = v) and lane
   // 16 + m (log-std head, n = 4 + v) of tile rt: bring row `lane` to lane
   // `lane` (rt = g) for the per-row sampling below

@@ -83,17 +83,27 @@ class BatchedActor(nn.Module):
         packed_features() zero-padded to a multiple of 4 floats; the biases b1
         [64], b2 [64], b3 [32]; then the MFMA A-operand fragments of fc1 (n_in
         zero-padded to 32 columns, 64 when n_in > 32), fc2, fc3 and the heads
-        (normal_head rows 0-3, log_std_head rows 4-7, zero rows to 16), each as
-        float4 [n-tile][k-quad][lane] = W[16 nt + lane % 16][16 q + 4 (lane // 16)
-        + 0..3] (the k order the kernel's chained MFMA layers sum in)."""
+        (normal_head rows 0-3, log_std_head rows 4-7, zero rows to 16) for
+        v_mfma_f32_16x16x32_bf16 with each weight split exactly into three
+        bfloat16 terms (w = hi + mid + lo, round-to-nearest each): per layer three
+        planes (hi, mid, lo) of bf16x8 [n-tile][k-pair p][lane], element j =
+        W[16 nt + lane % 16][32 p + 16 (j // 4) + 4 (lane // 16) + j % 4] (the k
+        order the kernel's chained layers sum in), stored as raw bits, two per
+        float."""
         n_in = self.layernorm.normalized_shape[0]
         dev = self.fc1.weight.device
 
         def frags(w, k_pad, n_pad):
             wp = torch.zeros((n_pad, k_pad), dtype=torch.float32, device=dev)
             wp[:w.shape[0], :w.shape[1]] = w.detach().float()
-            # [nt][m][q][g][v] -> [nt][q][lane = 16 g + m][v]
-            return wp.reshape(n_pad // 16, 16, k_pad // 16, 4, 4).permute(0, 2, 3, 1, 4).reshape(-1)
+            nt, qp = n_pad // 16, k_pad // 32
+            # [nt][m][p][half][g][v] -> [nt][p][lane = 16 g + m][j = 4 half + v]
+            x = wp.reshape(nt, 16, qp, 2, 4, 4).permute(0, 2, 4, 1, 3, 5).reshape(nt, qp, 64, 8)
+            hi = x.to(torch.bfloat16)
+            r = x - hi.float()
+            mid = r.to(torch.bfloat16)
+            lo = (r - mid.float()).to(torch.bfloat16)
+            return torch.stack([hi, mid, lo]).contiguous().reshape(-1).view(torch.float32)
 
         conv = self.packed_features()
         conv = torch.cat([conv, torch.zeros((-conv.numel()) % 4, device=dev)])

@@ -133,3 +133,46 @@ def test_observe_ex_strided_rows_and_null_side(name):
         g2.observe_into(-1, buf.data_ptr(), nb * Db - 4, None, 0)
     g1.close()
     g2.close()
+
+
+def test_policy_act_strided_input_equals_packed():
+    """lnw_policy_act reading its rows from a [E][T][n][D] rollout buffer at
+    step t (obs_in_env_stride) gives the outputs of the packed [E][n][D] rows,
+    and in place (obs_out == obs) leaves live envs' rows alone and zeroes the
+    ended ones."""
+    import ctypes as C
+    from lnw import _abi
+    from lnw.rollout import BatchedActor
+    L = _abi.load()
+    torch.manual_seed(7)
+    a = BatchedActor.for_obs(68).cuda()
+    E, n, D, T, t = 700, 4, 68, 6, 2
+    obs = torch.rand((E, n, D), device="cuda")
+    obs[:, :, :49] = torch.randint(0, 256, (E, n, 49), device="cuda") / 255.0
+    buf = torch.rand((E, T, n, D), device="cuda")
+    buf[:, t] = obs
+    act = torch.rand((E, n, 4), device="cuda")
+    alive = torch.ones((n, E), dtype=torch.uint8, device="cuda")
+    live = torch.ones(E, dtype=torch.uint8, device="cuda")
+    live[::5] = 0
+    params = a.packed_policy()
+    res = []
+    for strided in (False, True):
+        lp = torch.zeros((E, n, 4), device="cuda")
+        pa = _abi.PolicyArgs()
+        src = buf.data_ptr() + t * n * D * 4 if strided else obs.data_ptr()
+        pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = src, E, n, D, 0, n
+        pa.obs_in_env_stride = T * n * D if strided else 0
+        pa.params, pa.forced, pa.forced_act, pa.fa_env_stride = params.data_ptr(), 1, act.data_ptr(), n * 4
+        pa.alive, pa.logp_out, pa.act_env_stride = alive.data_ptr(), lp.data_ptr(), n * 4
+        pa.live = live.data_ptr()
+        if strided:
+            pa.obs_out, pa.obs_env_stride = src, T * n * D
+        _abi.check(L.lnw_policy_act(C.byref(pa), None))
+        torch.cuda.synchronize()
+        res.append(lp)
+    assert torch.equal(res[0], res[1])
+    keep = live.bool()
+    assert torch.equal(buf[keep, t], obs[keep]) and not buf[~keep, t].any()
+    others = [s for s in range(T) if s != t]
+    assert not (buf[:, others] == 0).all()

@@ -147,6 +147,26 @@ def _unpack_frags(F, nto, q):
     return W, nto * q * 256
 
 
+def _unpack_bf3(F, nto, q):
+    """The weight matrix of a layer packed for lnw_policy_act's bf16 MFMAs:
+    planes hi, mid, lo of bf16x8 [nt][p][lane], element j = W[16 nt + lane % 16]
+    [32 p + 16 (j // 4) + 4 (lane // 16) + j % 4]; hi + mid + lo is the f32
+    weight exactly."""
+    import numpy as np
+    import torch
+    n = 3 * nto * (q // 2) * 64 * 8 // 2  # floats (two bf16 each)
+    bits = torch.from_numpy(np.ascontiguousarray(F[:n])).view(torch.bfloat16).float().numpy()
+    fr = bits.reshape(3, nto, q // 2, 64, 8)
+    W = np.zeros((16 * nto, 16 * q), np.float32)
+    for lane in range(64):
+        m, g = lane % 16, lane // 16
+        for j in range(8):
+            k = np.arange(q // 2)[None, :] * 32 + 16 * (j // 4) + 4 * g + j % 4
+            # (hi + mid) + lo: each step exact (the split is)
+            W[np.arange(nto)[:, None] * 16 + m, k] = (fr[0, :, :, lane, j] + fr[1, :, :, lane, j]) + fr[2, :, :, lane, j]
+    return W, n
+
+
 def test_policy_packing_matches_layers():
     """BatchedActor.packed_policy / BatchedCritic.packed (the layouts
     lnw_policy_act / lnw_rollout_post read): the fragment runs decode back to
@@ -164,10 +184,10 @@ def test_policy_packing_matches_layers():
         b = P[conv:conv + 160]
         F = P[conv + 160:]
         k1 = 32 if n_in <= 32 else 64
-        W1, o = _unpack_frags(F, 4, k1 // 16)
-        W2, o2 = _unpack_frags(F[o:], 4, 4)
-        W3, o3 = _unpack_frags(F[o + o2:], 2, 4)
-        WH, o4 = _unpack_frags(F[o + o2 + o3:], 1, 2)
+        W1, o = _unpack_bf3(F, 4, k1 // 16)
+        W2, o2 = _unpack_bf3(F[o:], 4, 4)
+        W3, o3 = _unpack_bf3(F[o + o2:], 2, 4)
+        WH, o4 = _unpack_bf3(F[o + o2 + o3:], 1, 2)
         assert o + o2 + o3 + o4 == len(F)
         assert np.array_equal(W1[:, :n_in], a.fc1.weight.detach().numpy()) and not W1[:, n_in:].any()
         assert np.array_equal(W2, a.fc2.weight.detach().numpy())
