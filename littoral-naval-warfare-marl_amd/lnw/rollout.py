@@ -307,6 +307,12 @@ def gae(rewards, values, gamma, lambda_=0.95):
     return returns
 
 
+# The rollout's fast path observes into the buffer directly and the policy
+# reads the rows there (obs_in_env_stride); off: the rows go to the game's
+# packed observation buffer and the policy copies them.
+STRIDED_POLICY_INPUT = False
+
+
 class Rollout:
     """Batched MAPPO rollout (ppo.py:421-671, side being trained = blue): env e
     plays one rollout episode; all E envs advance together. Every step t:
@@ -443,17 +449,22 @@ class Rollout:
         # rows in place), red's only where a red actor reads them, and the step
         # writes none (ppo.py:577 discards them). g.obs_blue is not updated then.
         direct = self.observe == "fresh" and on_step is None
+        # (STRIDED_POLICY_INPUT: the policy reads the rows in the buffer itself)
+        strided = direct and STRIDED_POLICY_INPUT
         if self.observe == "step":
             g.observe(-1)
         for t in range(T):
             row_t = P(obs) + t * nb * Db * f4  # the rollout buffer's rows of step t
-            if direct:
-                g.observe_into(-1, row_t, T * nb * Db, P(g.obs_red) if red_actor_rows else None, 0)
+            red_rows = P(g.obs_red) if red_actor_rows else None
+            if strided:
+                g.observe_into(-1, row_t, T * nb * Db, red_rows, 0)
+            elif direct:
+                g.observe_into(-1, P(g.obs_blue), 0, red_rows, 0)
             elif self.observe == "fresh":
                 g.observe(-1)
             pa = PolicyArgs()
-            pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = (row_t if direct else P(g.obs_blue)), E, nb, Db, 0, A
-            pa.obs_in_env_stride = T * nb * Db if direct else 0
+            pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = (row_t if strided else P(g.obs_blue)), E, nb, Db, 0, A
+            pa.obs_in_env_stride = T * nb * Db if strided else 0
             pa.params, pa.bn_running = P(ap), int(self.bn == "running")
             if fa is not None:
                 pa.forced, pa.forced_act, pa.fa_env_stride = 1, P(fa) + t * A * 4 * f4, T * A * 4

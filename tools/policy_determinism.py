@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Diagnostics: lnw_policy_act called repeatedly on the same rows (packed, and
+strided in place like the rollout's direct path) -- are the outputs
+bit-identical from call to call?  usage: python tools/policy_determinism.py [E] [reps]"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "littoral-naval-warfare-marl_amd")]
+
+
+def main():
+    import torch
+    from lnw import _abi
+    from lnw.rollout import BatchedActor
+    path = os.environ.get("POLICY_LIB")
+    if path:  # an lnw_actor.hip-only build (tools/probe)
+        L = C.CDLL(path)
+        L.lnw_policy_act.argtypes = [C.POINTER(_abi.PolicyArgs), C.c_void_p]
+        print("lib", path, flush=True)
+    else:
+        L = _abi.load()
+    E = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    n, D, T, t = 4, 68, 40, 5
+    torch.manual_seed(0)
+    actor = BatchedActor.for_obs(D).cuda()
+    ap = actor.packed_policy()
+    obs = torch.rand((E, n, D), device="cuda")
+    obs[:, :, :49] = torch.randint(0, 256, (E, n, 49), device="cuda") / 255.0
+    buf = torch.zeros((E, T, n, D), device="cuda")
+    alive = torch.ones((2 * n, E), dtype=torch.uint8, device="cuda")
+    live = torch.ones(E, dtype=torch.bool, device="cuda")
+    call = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out2 = torch.zeros((E, T, n, D), device="cuda")
+    variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["packed", "strided", "strided_sync",
+                                                                   "strided_copy", "packed_inplace"]
+    for var in variants:
+        strided = var.startswith("strided")
+        ref = None
+        nd = 0
+        for k in range(reps):
+            buf[:, t] = obs
+            if var == "strided_sync":
+                torch.cuda.synchronize()
+            acts = torch.zeros((E, T, n, 4), device="cuda")
+            logp = torch.zeros((E, T, n, 4), device="cuda")
+            full = torch.zeros((E, 2 * n, 4), dtype=torch.float64, device="cuda")
+            pa = _abi.PolicyArgs()
+            src = buf.data_ptr() + t * n * D * 4 if strided else obs.data_ptr()
+            pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = src, E, n, D, 0, 2 * n
+            pa.obs_in_env_stride = T * n * D if strided else 0
+            pa.params, pa.noise, pa.seed, pa.call_dev, pa.T, pa.t = ap.data_ptr(), 0.05, 99, call.data_ptr(), T, t
+            pa.alive, pa.live = alive.data_ptr(), live.data_ptr()
+            pa.obs_out, pa.obs_env_stride = buf.data_ptr() + t * n * D * 4, T * n * D
+            if var == "strided_copy":
+                pa.obs_out = out2.data_ptr() + t * n * D * 4
+            if var == "packed_inplace":
+                pa.obs_out, pa.obs_env_stride = obs.data_ptr(), n * D
+            if var == "strided_nolive":
+                pa.live = None
+            if var == "strided_noout":
+                pa.obs_out = None
+            pa.act_out, pa.logp_out, pa.act_env_stride = acts.data_ptr() + t * n * 16, logp.data_ptr() + t * n * 16, T * n * 4
+            pa.full = full.data_ptr()
+            assert L.lnw_policy_act(C.byref(pa), None) == 0
+            torch.cuda.synchronize()
+            cur = (acts[:, t].clone(), logp[:, t].clone(), full.clone())
+            if ref is None:
+                ref = cur
+                continue
+            for name, x, y in zip(("act", "logp", "full"), cur, ref):
+                if not torch.equal(x, y):
+                    d = (x != y).nonzero()
+                    nd += 1
+                    if nd <= 3:
+                        print(var, "rep", k, name, int((x != y).sum()), "differ, e.g.", d[0].tolist(),
+                              float(x[tuple(d[0])]), float(y[tuple(d[0])]), flush=True)
+        print(var, "mismatching (rep, output) pairs:", nd, "of", 3 * (reps - 1), flush=True)
+
+
+if __name__ == "__main__":
+    main()
