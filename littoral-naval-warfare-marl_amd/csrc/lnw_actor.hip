@@ -86,6 +86,12 @@ __device__ __forceinline__ void conv_head_row(const float *P, const float *x, fl
   float win[WIN];
 #pragma unroll
   for (int i = 0; i < WIN; i++) win[i] = x[i];
+  // every load of the row done before any use: around these loads the
+  // compiler spills registers to scratch and its partial vmcnt waits then do
+  // not hold (a row spread over distant lines, e.g. in a rollout buffer, read
+  // a register before its load landed: tools/policy_determinism.py; the
+  // strided policy input stays off for the same reason, rollout.py)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // conv1 (1 -> 5, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (7x7 -> 3x3),
   // one channel at a time (rolled: 49 outputs live)
 #pragma unroll 1

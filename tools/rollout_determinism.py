@@ -35,14 +35,24 @@ def main():
         plain(*args, **kw)
         torch.cuda.synchronize()
     modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["direct", "direct", "callback", "direct"]
-    for mode in modes:
+    for mode in [m for m in modes if m != "graph"]:
         g.set_state(snap)
         r.call_index(7)
         cb = (lambda t, out: None) if mode == "callback" else None
         g.observe_into = synced if mode == "sync" else plain
+        import lnw.rollout as lr
+        lr.STRIDED_POLICY_INPUT = mode == "strided"
         o = {k: v.clone() for k, v in r.run(on_step=cb).items() if v is not None}
         torch.cuda.synchronize()
         outs.append((mode, o, g.get_state()))
+    if "graph" in modes or len(sys.argv) > 5:
+        r.capture()
+        for k in range(int(sys.argv[5]) if len(sys.argv) > 5 else 2):
+            g.set_state(snap)
+            r.call_index(7)
+            o = {k2: v.clone() for k2, v in r.replay().items() if v is not None}
+            torch.cuda.synchronize()
+            outs.append(("graph", o, g.get_state()))
     base = outs[0]
     for mode, o, st in outs[1:]:
         bad = []
