@@ -55,7 +55,7 @@ struct KParams {
   int atan_odd;       // the host's bearing table is odd in dy (degrees(atan2(-dy, dx)) == -degrees(atan2(dy, dx))): the group kernel stages its dy >= 0 half
   int no_obs;         // lnw_step without observation outputs (both pointers NULL)
   long long obs_stride[2];  // lnw_observe_ex: floats between envs' rows per side (0: packed)
-  int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table, bit13 4-ship phase-S rows stored row by row instead of line-aligned
+  int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table, bit13 4-ship phase-S rows stored row by row instead of line-aligned, bit15 the group kernel's fire loop entry by entry
 };
 
 // Device state (SoA, agent-major [field][agent][env] so a wave of envs reads
@@ -323,6 +323,18 @@ struct Rng {
     ctr += 2;
     u1 = u53(o1[0], o1[1]);
     u2 = u53(o2[0], o2[1]);
+  }
+  // the uniform draw with draw number c, without touching the cursor or the
+  // error bits (the caller accounts for both: fire_group_chunk); a tape
+  // position past the end reads 0.0, as tnext
+  __device__ __forceinline__ double uniform_at(unsigned long long c) const {
+    if (mode == 1) {
+      const long long p = tape_lo + (long long)c;
+      return p < tape_hi ? tape[p] : 0.0;
+    }
+    uint32_t o[4] = {(uint32_t)c, (uint32_t)(c >> 32), g0, g1};
+    philox10(o, k0, k1);
+    return u53(o[0], o[1]);
   }
   __device__ double gauss() {
     if (mode == 1) return tnext();

@@ -3844,11 +3844,12 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   if (const char *dbg = getenv("LNW_DEBUG_SKIP")) h->dbg_skip = atoi(dbg);
 #ifndef LNW_DIAG
   // the shipped library honours only the knobs that change the launch shape or
-  // code path, never the results (bit 9: no quiet path, 17: per-lane bearing
-  // loop, 22/23: where the head's loads are issued); section skips and
+  // code path, never the results (bit 9: no quiet path, 15: the group kernel's
+  // fire loop entry by entry, 17: per-lane bearing loop, 22/23: where the
+  // head's loads are issued); section skips and
   // replaced arithmetic exist only in the diagnostics build (-DLNW_DIAG,
   // lnw.build.build_diag)
-  constexpr int kResultPreserving = 512 | 131072 | 4194304 | 8388608;
+  constexpr int kResultPreserving = 512 | 32768 | 131072 | 4194304 | 8388608;
   if (h->dbg_skip & ~kResultPreserving) {
     const int bad = h->dbg_skip & ~kResultPreserving;
     delete h;
