@@ -1302,13 +1302,14 @@ __device__ __forceinline__ void get_obs_walk_t(Ctx &X, int me, int own0, int opp
 // order, and pair b of column j yields a bearing iff b is in EW and b < f.
 // Bearings, gauss draws and fixes then run in finish_obs_t.
 template <int NOWN, int NOPP>
-__device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp0) {
+__device__ __forceinline__ void mask_walk_t(Ctx &X, int me, int own0, int opp0, uint32_t (&pp)[NOPP],
+                                            uint32_t &amask, uint32_t &firstbit, uint32_t &bearm) {
   static_assert(NOWN * NOPP <= 16, "pair masks are 16 bits");
   Cols &c = X.c;
   const int lane = X.lane;
   const int myradar = COLW(c.radar_cur, me);
-  uint32_t pp[NOPP];
-  uint32_t amask = 0, rowsel = 0;
+  uint32_t rowsel = 0;
+  amask = 0;
 #pragma unroll
   for (int i = 0; i < NOWN; i++) {
     // own ship i stands on its new cell once its turn has come and it moved
@@ -1329,7 +1330,8 @@ __device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp
   uint32_t colj = 0;  // bits of opponent 0's column
 #pragma unroll
   for (int i = 0; i < NOWN; i++) colj |= 1u << (i * NOPP);
-  uint32_t firstbit = 0, bearm = 0;  // bit b: pair b appends to observed / takes a bearing
+  firstbit = 0;  // bit b: pair b appends to observed / takes a bearing
+  bearm = 0;
 #pragma unroll
   for (int j = 0; j < NOPP; j++) {
     uint32_t cls = 0;  // columns of the opponents on j's cell (observed is de-duplicated by cell)
@@ -1341,6 +1343,12 @@ __device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp
     bearm |= ewm & (colj << j) & (f ? f - 1u : 0xffffffffu);
   }
   prof_acc(X.S, 20, tw);
+}
+
+template <int NOWN, int NOPP>
+__device__ __forceinline__ void get_obs_mask_t(Ctx &X, int me, int own0, int opp0) {
+  uint32_t pp[NOPP], amask, firstbit, bearm;
+  mask_walk_t<NOWN, NOPP>(X, me, own0, opp0, pp, amask, firstbit, bearm);
   finish_obs_t<NOWN, NOPP, true>(X, me, own0, opp0, 0, firstbit, bearm, pp, amask >> NOWN);
 }
 
@@ -3155,10 +3163,21 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
 // one batch (los_prefetch_t: no ship moves here, so only the current cells) and
 // the templated get_obs (get_obs_t; CW: the contact variant's mask walk), as
 // the step kernel's phase S; NB = NR = 0: runtime sizes (get_obs_dev).
+// CW with compile-time sizes: two waves, blue's calls on wave 0 and red's on
+// wave 1. No ship moves and a call changes only its own ship's target list, so
+// the calls are independent but for the draw counter: blue's calls take their
+// draws first, and a call takes one draw per bearing of its walk. Wave 1 runs
+// blue's walks alone (register bit arithmetic, no draws) to count them, starts
+// red's calls past them, and keeps its pooled-bearing tables in the actions'
+// LDS columns (unused here); the env's final counter and error bits are merged
+// after a barrier. (The EW-fix log, whose records keep the calls' order, and a
+// single side or ship keep the calls on wave 0.)
 template <int NB = 0, int NR = 0, bool CW = false>
-__global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int sel, float *obs_b,
-                                                     float *obs_r) {
+__global__ __launch_bounds__(NB > 0 && CW ? 2 * WAVE : WAVE) void observe_kernel(KParams P, KState S, int sel,
+                                                                                 float *obs_b, float *obs_r) {
+  constexpr int NW = NB > 0 && CW ? 2 : 1;
   const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = NW > 1 ? (int)(threadIdx.x / WAVE) : 0;
   const int epw = P.epw;
   const int env0 = xcd_chunk(P, (int)blockIdx.x, (int)gridDim.x) * epw;
   const int env = env0 + lane;
@@ -3169,25 +3188,52 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
   LdsLayout L = lds_layout(A, P.nb, P.nr, S.nmax, P.G * P.W16, P.G);
   Cols c = carve(lds_dyn, L);
   __shared__ double duct_col[WAVE];
-  for (int w = lane; w < P.G * P.W16; w += WAVE) c.mask[w] = S.mask2[w];
+  __shared__ unsigned long long ctr1[NW > 1 ? WAVE : 1];  // wave 1's final draw counter and error bits
+  __shared__ uint32_t err1[NW > 1 ? WAVE : 1];
+  for (int w = (int)threadIdx.x; w < P.G * P.W16; w += NW * WAVE) c.mask[w] = S.mask2[w];
   const uint32_t *mask = c.mask;
-  load_state<NB + NR, 1>(P, S, c, lane, env, valid, 0);
+  load_state<NB + NR, NW>(P, S, c, lane, env, valid, wid);
   double duct = valid ? S.duct[env] : 1.0;
-  duct_col[lane] = duct;
+  if (wid == 0) duct_col[lane] = duct;
   __syncthreads();
+  int a0 = 0, a1 = A;
+  if (sel >= 0) { a0 = sel; a1 = sel + 1; }
+  else if (sel == LNW_OBS_BLUE) { a1 = nb; }
+  else if (sel == LNW_OBS_RED) { a0 = nb; }
+  const bool split = NW > 1 && sel == LNW_OBS_ALL && !S.ana.ew_log;
+  int wa0 = a0, wa1 = a1;  // this wave's calls
+  if (NW > 1) {
+    if (split) { wa0 = wid ? nb : 0; wa1 = wid ? A : nb; }
+    else if (wid == 1) { wa1 = wa0; }
+  }
+  unsigned long long fctr = 0;
+  uint32_t ferr = 0;
   if (valid) {
-    Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), mask, E, max_range2(P, duct),
+    Cols cw = c;
+    if (NW > 1 && wid == 1) cw.observed = (uint32_t *)(lds_dyn + L.act0);
+    Ctx X{P, S, cw, lane, env, duct_col, make_rng(P, S, env), mask, E, max_range2(P, duct),
           S.envi[2 * E + env]};
-    int a0 = 0, a1 = A;
-    if (sel >= 0) { a0 = sel; a1 = sel + 1; }
-    else if (sel == LNW_OBS_BLUE) { a1 = nb; }
-    else if (sel == LNW_OBS_RED) { a0 = nb; }
     if constexpr (NB > 0 && CW) {
       pair_tables_t<NB, NR, false>(X);
+      if (split && wid == 1) {  // past blue's draws
+        long long nd = 0;
+        for (int a = 0; a < nb; a++) {
+          if (!COLB(c.alive0, a)) continue;
+          uint32_t pp[NR], am, fb, bm;
+          mask_walk_t<NB, NR>(X, a, 0, NB, pp, am, fb, bm);
+          nd += __builtin_popcount(bm);
+        }
+        if (X.rng.mode == 1) {  // a tape stops at its end (blue's calls flag it)
+          const long long len = X.rng.tape_hi - X.rng.tape_lo, cur = (long long)X.rng.ctr;
+          X.rng.ctr = (unsigned long long)(cur + nd <= len ? cur + nd : (cur > len ? cur : len));
+        } else {
+          X.rng.ctr += (unsigned long long)nd;
+        }
+      }
     } else if constexpr (NB > 0) {
       if (P.los_mode != 1) los_prefetch_t<NB, NR>(X);
     }
-    for (int a = a0; a < a1; a++) {
+    for (int a = wa0; a < wa1; a++) {
       if (!COLB(c.alive0, a)) continue;
       if constexpr (NB > 0) {
         if (a < NB) get_obs_t<NB, NR, CW>(X, a, 0, NB);
@@ -3199,10 +3245,26 @@ __global__ __launch_bounds__(64) void observe_kernel(KParams P, KState S, int se
       COLB(c.obsd, a) = 1;
       S.tl_cnt[(size_t)a * E + env] = (uint16_t)COLW(c.tcnt, a);
     }
-    S.rng[env] = X.rng.ctr;
-    if (X.rng.err) S.err[env] |= X.rng.err;
+    fctr = X.rng.ctr;
+    ferr = X.rng.err;
+    if (NW > 1 && wid == 1) {
+      ctr1[lane] = split ? fctr : 0ull;
+      err1[lane] = ferr;
+    }
   }
-  __syncthreads();
+  if constexpr (NW > 1) {
+    __syncthreads();
+    if (wid == 1) return;
+    if (valid) {  // (counters only grow: wave 1 started where wave 0 ends)
+      fctr = fctr > ctr1[lane] ? fctr : ctr1[lane];
+      ferr |= err1[lane];
+    }
+  }
+  if (valid) {
+    S.rng[env] = fctr;
+    if (ferr) S.err[env] |= ferr;
+  }
+  if constexpr (NW == 1) __syncthreads();
   // rows of ships not observed in this call are written as zeros
   write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, true);
 }
@@ -4240,8 +4302,9 @@ int lnw_observe_ex(lnw_handle *h, int32_t agent, float *obs_blue_dev, int64_t bl
   KParams k = h->kp;
   k.obs_stride[0] = blue_env_stride;
   k.obs_stride[1] = red_env_stride;
-#define LNW_OBS(NB_, CW_) \
-  observe_kernel<NB_, NB_, CW_><<<grid, block, lds, st>>>(k, s, agent, obs_blue_dev, obs_red_dev)
+#define LNW_OBS(NB_, CW_)                                                                          \
+  observe_kernel<NB_, NB_, CW_><<<grid, dim3(NB_ > 0 && CW_ ? 2 * WAVE : WAVE), lds, st>>>(k, s, agent, \
+                                                                                    obs_blue_dev, obs_red_dev)
   if (tmpl && h->nb == 4) { if (cw) LNW_OBS(4, true); else LNW_OBS(4, false); }
   else if (tmpl && h->nb == 3) { if (cw) LNW_OBS(3, true); else LNW_OBS(3, false); }
   else if (tmpl && h->nb == 2) { if (cw) LNW_OBS(2, true); else LNW_OBS(2, false); }
