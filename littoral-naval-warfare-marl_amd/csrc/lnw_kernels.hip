@@ -1303,11 +1303,13 @@ __device__ __forceinline__ void get_obs_walk_t(Ctx &X, int me, int own0, int opp
 // Bearings, gauss draws and fixes then run in finish_obs_t.
 template <int NOWN, int NOPP>
 __device__ __forceinline__ void mask_walk_t(Ctx &X, int me, int own0, int opp0, uint32_t (&pp)[NOPP],
-                                            uint32_t &amask, uint32_t &firstbit, uint32_t &bearm) {
+                                            uint32_t &amask, uint32_t &firstbit, uint32_t &bearm,
+                                            bool radv_set = false, int radv = 0) {
   static_assert(NOWN * NOPP <= 16, "pair masks are 16 bits");
   Cols &c = X.c;
   const int lane = X.lane;
-  const int myradar = COLW(c.radar_cur, me);
+  // (radv: the observer's radar as take_action sets it, for a walk counted ahead of its turn)
+  const int myradar = radv_set ? radv : COLW(c.radar_cur, me);
   uint32_t rowsel = 0;
   amask = 0;
 #pragma unroll
@@ -1710,6 +1712,48 @@ __device__ inline bool fire_dev(Ctx &X, int a, int tx, int ty, double salvo, int
     N.mask[ts] |= 1u << (t - (ts ? P.nb : 0));
   }
   return hit;
+}
+
+// The draws take_action's fire loop over ship a's previous target list takes
+// (fire_dev without its draws: two per missile shot, combatant.py:612, 630),
+// counted ahead of the turn: the targets are found among the opponents' start
+// cells and alive flags, and the missile count runs its recurrence.
+__device__ inline int fire_draws(Ctx &X, int a, double salvo, int ksalvo) {
+  const KParams &P = X.P;
+  Cols &c = X.c;
+  const int lane = X.lane;
+  const int side = a >= P.nb;
+  const int tn = (int)COLW(c.tcnt, a);
+  int miss = COLB(c.miss_cur, a), mk = COLB(c.mkind, a), nd = 0;
+  const uint16_t *tl = X.S.tl + (size_t)a * P.T * X.E + X.env;
+  const uint32_t pa = COLW(c.pos_cur, a);
+  for (int q = 0; q < tn; q++) {
+    const uint16_t tg = tl[(size_t)q * X.E];
+    const int t = check_target_dev<false>(X, side, tg & 0xff, tg >> 8);
+    if (t < 0) continue;
+    const uint32_t pt = COLW(c.pos_cur, t);
+    const int dx = pos_x(pt) - pos_x(pa), dy = pos_y(pt) - pos_y(pa);
+    if (dx * dx + dy * dy < 4 || miss == 0) continue;  // main gun, or no missiles: no draw
+    double num;
+    int kn;
+    if (!P.discrete) {
+      if (kind_promote(mk, ksalvo) == K_F32) {
+        num = (double)rintf((float)miss * (float)salvo);
+        kn = K_F32;
+      } else {
+        num = rint((double)miss * salvo);
+        kn = K_F64;
+      }
+    } else {
+      num = COLB(c.type, a) == T_SMALL ? salvo : salvo * 2.0;
+      kn = K_PYINT;
+    }
+    if (num > (double)miss) { num = (double)miss; kn = mk; }
+    miss = (miss - (int)num) & 0xff;
+    mk = kind_promote(mk, kn);
+    nd += 2;
+  }
+  return nd;
 }
 
 // calculate_reward (game.py:214-295) for agent a of the env in LDS column `lane`
@@ -2881,7 +2925,7 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // observation passes go through one workgroup-wide queue that every free wave
 // of a quiet unit serves, so the CU's units finish their stream together
 // instead of 4-5 us apart (the spread of separate workgroups on one CU).
-template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1>
+template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false>
 __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
@@ -3000,7 +3044,26 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
       if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
     }
   }
-  if (wid == 1) {
+  // The contact variant without observation rows (lnw_step with NULL outputs:
+  // the MAPPO rollout's step) leaves wave 1 free after phase M. Phase S then
+  // splits by side (templated 4v4, loud workgroups): wave 0 plays blue's turns
+  // and wave 1 red's. Red's turns read blue only at its final cells and radars
+  // (known after phase M — the moves, and radar = rint(a0)), and
+  // blue's read red at its start cells and radars, so each wave works on its own
+  // view of the cells and radars (wave 1's copy: blue final, red at the start,
+  // in the emission stage's LDS, unused without rows). What ties the sides
+  // together is the draw counter: wave 1 counts blue's draws first — the fire
+  // loops' missile shots before a barrier (blue's get_obs then rewrites those
+  // lists), the get_obs walks' bearings after it — and starts red's turns past
+  // them. After a second barrier wave 0 merges red's hits, sums, counter and
+  // cells and runs the tail. (The engagement and EW-fix logs, whose records keep
+  // the turn order, keep phase S on wave 0.)
+  // (a separate instantiation, PS, so the contact variant's row-writing kernel
+  // keeps its code)
+  const bool psplit = PS && CW && NB == 4 && NR == 4 && UN == 1 && EPW == WAVE && P.no_obs &&
+                      P.los_mode == 0 && !(P.dbg_skip & 515) && !S.ana.eng_log && !S.ana.ew_log &&
+                      !(P.dbg_skip & 16384);
+  if (wid == 1 && !psplit) {
     if constexpr (ST) {
       if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
     }
@@ -3008,7 +3071,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
     return;
   }
   if (!qcap && astar && !(P.dbg_skip & 4)) {
-    // the rare A* fallback (open lists sized for one wave)
+    // the rare A* fallback (open lists sized for one wave; psplit implies qcap)
     move_astar_pass(P, S, c, nenv, A);
     wave_lds_sync();
   }
@@ -3017,7 +3080,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   prof_stamp(S, 1);
   if (valid && !(P.dbg_skip & 2)) {
     if (emit) publish_progress(&prog, 0);
-    Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), emit ? S.mask2 : mask, E,
+    Ctx X{P, S, c, lane, env, duct_col, make_rng(P, S, env), (emit || psplit) ? S.mask2 : mask, E,
           r2col[lane], 0};
     unsigned long long tp[4] = {0, 0, 0, 0}, t0 = prof_now(S);  // LNW_PROF part totals
     if constexpr (ST && CW) {
@@ -3034,112 +3097,331 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
     int hits[2] = {0, 0};
     int bsx = 0, bsy = 0, rsx = 0, rsy = 0;  // exact integer sums
     int nbp = 0, nrp = 0;
-    // each agent in three sections that reconverge (take_action up to the move,
-    // get_obs, reward), so the LNW_PROF section timers measure the wave
-    for (int a = 0; a < A; a++) {
-      const bool al = COLB(c.alive0, a) != 0;  // sunk ships skip their turn (reward 0)
-      const int side = a >= nb;
-      bool engage = false, moved = false;
-      int destroyed = 0;
-      t0 = prof_now(S);
-      if (al) {
-        uint32_t p0 = COLW(c.pos_cur, a);
-        if (!side) {
-          if (P.side_blue) { bsx += pos_x(p0); bsy += pos_y(p0); nbp++; }
-        } else {
-          rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
-        }
-        size_t row = ((size_t)env * A + a) * 4;
-        double a0 = COLW(c.act0, a), a1 = COLW(c.act1, a);
-        int kind = COLB(c.akind, a);
-        // untrained red: random salvo (game.py:375-379), written back in place
-        if (side && !P.trained_red) {
-          if (X.rng.uniform() < P.red_aggression) {
-            double v = X.rng.uniform();
-            if (dt == LNW_ACT_F32) { float f = (float)v; ((float *)actions)[row + 1] = f; a1 = f; }
-            else if (dt == LNW_ACT_F64) {
-              if (kind == K_F32) v = (double)(float)v;
-              ((double *)actions)[row + 1] = v; a1 = v;
-            } else { ((int32_t *)actions)[row + 1] = 0; a1 = 0.0; }
+    if constexpr (PS && ST && CW && NB == 4 && NR == 4) {
+      // one ship's turn (take_action, get_obs, calculate_reward: game.py:338-381)
+      // on the view X.c: wave 0's is the workgroup's columns, the split's wave 1
+      // its own (the parameters shadow the loop state they update)
+      // (the hit state is copied in and out: a runtime index into an array behind a
+      // reference would keep it in scratch)
+      auto turn = [&](Ctx &X, int a, Neut &Nio, int (&evio)[8], int (&hio)[2], int &bsx, int &bsy, int &nbp,
+                      int &rsx, int &rsy, int &nrp, unsigned long long (&tp)[4], unsigned long long &t0) {
+        Cols &c = X.c;
+        Neut N = Nio;
+        int ev[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hits[2] = {0, 0};
+        const bool al = COLB(c.alive0, a) != 0;  // sunk ships skip their turn (reward 0)
+        const int side = a >= nb;
+        bool engage = false, moved = false;
+        int destroyed = 0;
+        t0 = prof_now(S);
+        if (al) {
+          uint32_t p0 = COLW(c.pos_cur, a);
+          if (!side) {
+            if (P.side_blue) { bsx += pos_x(p0); bsy += pos_y(p0); nbp++; }
+          } else {
+            rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
           }
-        }
-        // take_action (combatant.py:501-565)
-        double engagement = P.discrete ? rint(a1) : a1;
-        int keng = P.discrete ? K_PYINT : kind;
-        int mk = COLB(c.mkind, a);
-        double thr_v;
-        if (kind_promote(keng, mk) == K_F32)
-          thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
-        else
-          thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
-        engage = thr_v > 0.0;
-        int tn = (int)COLW(c.tcnt, a);
-        if (engage && tn > 0 && !(P.dbg_skip & 65536)) {  // (bit 16: diagnostics, no fire)
-          const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
-          if constexpr (CW) {
-            // contact variant: the list read 8 entries at a time, the loads of a
-            // chunk in flight together (packed in a register pair: a runtime index
-            // into a register array would put it in scratch)
-            for (int q0 = 0; q0 < tn; q0 += 8) {
-              uint64_t pk0 = 0, pk1 = 0;
+          size_t row = ((size_t)env * A + a) * 4;
+          double a0 = COLW(c.act0, a), a1 = COLW(c.act1, a);
+          int kind = COLB(c.akind, a);
+          // untrained red: random salvo (game.py:375-379), written back in place
+          if (side && !P.trained_red) {
+            if (X.rng.uniform() < P.red_aggression) {
+              double v = X.rng.uniform();
+              if (dt == LNW_ACT_F32) { float f = (float)v; ((float *)actions)[row + 1] = f; a1 = f; }
+              else if (dt == LNW_ACT_F64) {
+                if (kind == K_F32) v = (double)(float)v;
+                ((double *)actions)[row + 1] = v; a1 = v;
+              } else { ((int32_t *)actions)[row + 1] = 0; a1 = 0.0; }
+            }
+          }
+          // take_action (combatant.py:501-565)
+          double engagement = P.discrete ? rint(a1) : a1;
+          int keng = P.discrete ? K_PYINT : kind;
+          int mk = COLB(c.mkind, a);
+          double thr_v;
+          if (kind_promote(keng, mk) == K_F32)
+            thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
+          else
+            thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
+          engage = thr_v > 0.0;
+          int tn = (int)COLW(c.tcnt, a);
+          if (engage && tn > 0 && !(P.dbg_skip & 65536)) {  // (bit 16: diagnostics, no fire)
+            const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
+            if constexpr (CW) {
+              // contact variant: the list read 8 entries at a time, the loads of a
+              // chunk in flight together (packed in a register pair: a runtime index
+              // into a register array would put it in scratch)
+              for (int q0 = 0; q0 < tn; q0 += 8) {
+                uint64_t pk0 = 0, pk1 = 0;
 #pragma unroll
-              for (int u = 0; u < 8; u++) {
-                const uint64_t v = q0 + u < tn ? (uint64_t)tl[(size_t)(q0 + u) * E] : 0ull;
-                if (u < 4) pk0 |= v << (16 * u);
-                else pk1 |= v << (16 * (u - 4));
+                for (int u = 0; u < 8; u++) {
+                  const uint64_t v = q0 + u < tn ? (uint64_t)tl[(size_t)(q0 + u) * E] : 0ull;
+                  if (u < 4) pk0 |= v << (16 * u);
+                  else pk1 |= v << (16 * (u - 4));
+                }
+                const int nq = tn - q0 < 8 ? tn - q0 : 8;
+                for (int u = 0; u < nq; u++) {
+                  const uint16_t tg = (uint16_t)((u < 4 ? pk0 : pk1) >> (16 * (u & 3)));
+                  if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+                }
               }
-              const int nq = tn - q0 < 8 ? tn - q0 : 8;
-              for (int u = 0; u < nq; u++) {
-                const uint16_t tg = (uint16_t)((u < 4 ? pk0 : pk1) >> (16 * (u & 3)));
+            } else {
+              uint16_t nx = tl[0];  // the next target's load is in flight while one fires
+              for (int q = 0; q < tn; q++) {
+                const uint16_t tg = nx;
+                if (q + 1 < tn) nx = tl[(size_t)(q + 1) * E];
                 if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
               }
             }
+          }
+          if (side) ev[6] += destroyed; else ev[5] += destroyed;
+          if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
+          else {
+            double rr = rint(a0);
+            COLW(c.radar_cur, a) = (int)fmin(fmax(rr, -2147483648.0), 2147483647.0);
+          }
+          uint32_t pn = COLW(c.pos_new, a);
+          moved = (pn & 0x80000000u) != 0;
+          if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
+        }
+        tp[0] += prof_now(S) - t0;
+        t0 = prof_now(S);
+        if (al && !(P.dbg_skip & 128)) {
+          if constexpr (REFW) march_pairs_ref(X, a);
+          if constexpr (ST) {
+            if (!side) get_obs_t<NB, NR, CW>(X, a, 0, NB);
+            else get_obs_t<NR, NB, CW>(X, a, NB, 0);
           } else {
-            uint16_t nx = tl[0];  // the next target's load is in flight while one fires
-            for (int q = 0; q < tn; q++) {
-              const uint16_t tg = nx;
-              if (q + 1 < tn) nx = tl[(size_t)(q + 1) * E];
-              if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
-            }
+            get_obs_dev(X, a);
           }
         }
-        if (side) ev[6] += destroyed; else ev[5] += destroyed;
-        if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
-        else {
-          double rr = rint(a0);
-          COLW(c.radar_cur, a) = (int)fmin(fmax(rr, -2147483648.0), 2147483647.0);
+        tp[2] += prof_now(S) - t0;
+        t0 = prof_now(S);
+        double r = 0.0;
+        if (al && !(P.dbg_skip & 256)) r = reward_dev(X, a, moved, engage, destroyed);
+        COLW(c.reward, a) = r;
+        if (al) {
+          if (!side) {
+            if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
+          } else {
+            if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
+          }
+          hits[side] += destroyed;
         }
-        uint32_t pn = COLW(c.pos_new, a);
-        moved = (pn & 0x80000000u) != 0;
-        if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
-      }
-      tp[0] += prof_now(S) - t0;
-      t0 = prof_now(S);
-      if (al && !(P.dbg_skip & 128)) {
-        if constexpr (REFW) march_pairs_ref(X, a);
-        if constexpr (ST) {
-          if (!side) get_obs_t<NB, NR, CW>(X, a, 0, NB);
-          else get_obs_t<NR, NB, CW>(X, a, NB, 0);
+        tp[3] += prof_now(S) - t0;
+        Nio = N;
+        evio[5] += ev[5];
+        evio[6] += ev[6];
+        hio[0] += hits[0];
+        hio[1] += hits[1];
+      };
+      if (psplit) {
+        // wave 1's view: pos / radar copies and its pooled-bearing tables in the
+        // emission stage (2 x 2 080 + 1 216 B of its >= 5 520)
+        Cols cr = c;
+        cr.pos_cur = (uint32_t *)(lds_dyn + L.mask);
+        cr.radar_cur = (int32_t *)(lds_dyn + L.mask + A * PAD * 4);
+        cr.observed = (uint32_t *)(lds_dyn + L.mask + 2 * A * PAD * 4);
+        long long nd = 0;  // blue's draws (wave 1)
+        if (wid == 1) {
+#pragma unroll
+          for (int a = 0; a < A; a++) {
+            uint32_t p = COLW(c.pos_cur, a);
+            int r = COLW(c.radar_cur, a);
+            if (a < NB && COLB(c.alive0, a)) {  // blue's final cell and radar
+              const uint32_t pn = COLW(c.pos_new, a);
+              if (pn & 0x80000000u) p = pn & 0x7fffffffu;
+              const double a0 = COLW(c.act0, a);
+              r = !isfinite(a0) ? 0 : (int)fmin(fmax(rint(a0), -2147483648.0), 2147483647.0);
+            }
+            COLW(cr.pos_cur, a) = p;
+            COLW(cr.radar_cur, a) = r;
+          }
+          for (int a = 0; a < NB; a++) {  // fire loops, before blue's get_obs rewrites the lists
+            if (!COLB(c.alive0, a)) continue;
+            const double a1 = COLW(c.act1, a);
+            const int kind = COLB(c.akind, a);
+            const double engagement = P.discrete ? rint(a1) : a1;
+            const int keng = P.discrete ? K_PYINT : kind;
+            const int mk = COLB(c.mkind, a);
+            const double thr_v = kind_promote(keng, mk) == K_F32
+                                     ? (double)rintf((float)engagement * (float)COLB(c.miss_cur, a))
+                                     : rint(engagement * (double)COLB(c.miss_cur, a));
+            if (thr_v > 0.0 && COLW(c.tcnt, a) > 0 && !(P.dbg_skip & 65536))
+              nd += fire_draws(X, a, engagement, keng);
+          }
+        }
+        __syncthreads();
+        if (wid == 1) {
+#pragma unroll
+          for (int a = 0; a < NB; a++) {  // get_obs walks (their bearings), radar as take_action sets it
+            if (!COLB(c.alive0, a)) continue;
+            uint32_t pp[NR], am, fb, bm;
+            mask_walk_t<NB, NR>(X, a, 0, NB, pp, am, fb, bm, true, COLW(cr.radar_cur, a));
+            nd += __builtin_popcount(bm);
+          }
+          Ctx Y{P, S, cr, lane, env, duct_col, X.rng, S.mask2, E, r2col[lane], X.step};
+          Y.ptr_[0] = X.ptr_[0]; Y.ptr_[1] = X.ptr_[1];
+          Y.ptc[0] = X.ptc[0]; Y.ptc[1] = X.ptc[1];
+          Y.ptw[0] = X.ptw[0]; Y.ptw[1] = X.ptw[1];
+          Y.pre = X.pre;
+          Y.lpre[0] = X.lpre[0]; Y.lpre[1] = X.lpre[1];
+          if (Y.rng.mode == 1) {  // a tape stops at its end (blue's turns flag it)
+            const long long len = Y.rng.tape_hi - Y.rng.tape_lo, cur = (long long)Y.rng.ctr;
+            Y.rng.ctr = (unsigned long long)(cur + nd <= len ? cur + nd : (cur > len ? cur : len));
+          } else {
+            Y.rng.ctr += (unsigned long long)nd;
+          }
+          Neut NR_{{0, 0}, {0u, 0u}};
+          int evr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hr[2] = {0, 0}, zb = 0, zby = 0, znb = 0;
+          for (int a = NB; a < A; a++) turn(Y, a, NR_, evr, hr, zb, zby, znb, rsx, rsy, nrp, tp, t0);
+          // red's results into the copies' blue rows (dead now)
+          COLW(cr.pos_cur, 0) = (uint32_t)NR_.cnt[0] | (uint32_t)NR_.cnt[1] << 16;
+          COLW(cr.pos_cur, 1) = NR_.mask[0] | NR_.mask[1] << 16;
+          COLW(cr.pos_cur, 2) = (uint32_t)rsx | (uint32_t)rsy << 16;
+          COLW(cr.pos_cur, 3) = (uint32_t)nrp | (uint32_t)hr[1] << 8;
+          COLW(cr.radar_cur, 0) = (int32_t)(uint32_t)Y.rng.ctr;
+          COLW(cr.radar_cur, 1) = (int32_t)(uint32_t)(Y.rng.ctr >> 32);
+          COLW(cr.radar_cur, 2) = (int32_t)Y.rng.err;
         } else {
-          get_obs_dev(X, a);
+          for (int a = 0; a < NB; a++) turn(X, a, N, ev, hits, bsx, bsy, nbp, rsx, rsy, nrp, tp, t0);
+        }
+        __syncthreads();
+        if (wid == 1) return;
+        {
+          const uint32_t w0 = COLW(cr.pos_cur, 0), w1 = COLW(cr.pos_cur, 1), w2 = COLW(cr.pos_cur, 2),
+                         w3 = COLW(cr.pos_cur, 3);
+          N.cnt[0] += (int)(w0 & 0xffffu);
+          N.cnt[1] += (int)(w0 >> 16);
+          N.mask[0] |= w1 & 0xffffu;
+          N.mask[1] |= w1 >> 16;
+          rsx = (int)(w2 & 0xffffu);
+          rsy = (int)(w2 >> 16);
+          nrp = (int)(w3 & 0xffu);
+          hits[1] += (int)(w3 >> 8);
+          ev[6] += (int)(w3 >> 8);
+          X.rng.ctr = (unsigned long long)(uint32_t)COLW(cr.radar_cur, 0) |
+                      (unsigned long long)(uint32_t)COLW(cr.radar_cur, 1) << 32;
+          X.rng.err |= (uint32_t)COLW(cr.radar_cur, 2);
+#pragma unroll
+          for (int a = NB; a < A; a++) {  // red's final cells and radars
+            COLW(c.pos_cur, a) = COLW(cr.pos_cur, a);
+            COLW(c.radar_cur, a) = COLW(cr.radar_cur, a);
+          }
+        }
+      } else {
+        for (int a = 0; a < A; a++) {
+          turn(X, a, N, ev, hits, bsx, bsy, nbp, rsx, rsy, nrp, tp, t0);
+          if (emit) publish_progress(&prog, a + 1);
+          if (a < 8) prof_stamp(S, 6 + a);
         }
       }
-      tp[2] += prof_now(S) - t0;
-      t0 = prof_now(S);
-      double r = 0.0;
-      if (al && !(P.dbg_skip & 256)) r = reward_dev(X, a, moved, engage, destroyed);
-      COLW(c.reward, a) = r;
-      if (al) {
-        if (!side) {
-          if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
-        } else {
-          if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
+    } else {  // (the loop written out: behind a lambda it keeps state in scratch)
+      for (int a = 0; a < A; a++) {
+        const bool al = COLB(c.alive0, a) != 0;  // sunk ships skip their turn (reward 0)
+        const int side = a >= nb;
+        bool engage = false, moved = false;
+        int destroyed = 0;
+        t0 = prof_now(S);
+        if (al) {
+          uint32_t p0 = COLW(c.pos_cur, a);
+          if (!side) {
+            if (P.side_blue) { bsx += pos_x(p0); bsy += pos_y(p0); nbp++; }
+          } else {
+            rsx += pos_x(p0); rsy += pos_y(p0); nrp++;
+          }
+          size_t row = ((size_t)env * A + a) * 4;
+          double a0 = COLW(c.act0, a), a1 = COLW(c.act1, a);
+          int kind = COLB(c.akind, a);
+          // untrained red: random salvo (game.py:375-379), written back in place
+          if (side && !P.trained_red) {
+            if (X.rng.uniform() < P.red_aggression) {
+              double v = X.rng.uniform();
+              if (dt == LNW_ACT_F32) { float f = (float)v; ((float *)actions)[row + 1] = f; a1 = f; }
+              else if (dt == LNW_ACT_F64) {
+                if (kind == K_F32) v = (double)(float)v;
+                ((double *)actions)[row + 1] = v; a1 = v;
+              } else { ((int32_t *)actions)[row + 1] = 0; a1 = 0.0; }
+            }
+          }
+          // take_action (combatant.py:501-565)
+          double engagement = P.discrete ? rint(a1) : a1;
+          int keng = P.discrete ? K_PYINT : kind;
+          int mk = COLB(c.mkind, a);
+          double thr_v;
+          if (kind_promote(keng, mk) == K_F32)
+            thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
+          else
+            thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
+          engage = thr_v > 0.0;
+          int tn = (int)COLW(c.tcnt, a);
+          if (engage && tn > 0 && !(P.dbg_skip & 65536)) {  // (bit 16: diagnostics, no fire)
+            const uint16_t *tl = S.tl + (size_t)a * P.T * E + env;
+            if constexpr (CW) {
+              // contact variant: the list read 8 entries at a time, the loads of a
+              // chunk in flight together (packed in a register pair: a runtime index
+              // into a register array would put it in scratch)
+              for (int q0 = 0; q0 < tn; q0 += 8) {
+                uint64_t pk0 = 0, pk1 = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                  const uint64_t v = q0 + u < tn ? (uint64_t)tl[(size_t)(q0 + u) * E] : 0ull;
+                  if (u < 4) pk0 |= v << (16 * u);
+                  else pk1 |= v << (16 * (u - 4));
+                }
+                const int nq = tn - q0 < 8 ? tn - q0 : 8;
+                for (int u = 0; u < nq; u++) {
+                  const uint16_t tg = (uint16_t)((u < 4 ? pk0 : pk1) >> (16 * (u & 3)));
+                  if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+                }
+              }
+            } else {
+              uint16_t nx = tl[0];  // the next target's load is in flight while one fires
+              for (int q = 0; q < tn; q++) {
+                const uint16_t tg = nx;
+                if (q + 1 < tn) nx = tl[(size_t)(q + 1) * E];
+                if (fire_dev(X, a, tg & 0xff, tg >> 8, engagement, keng, N)) destroyed++;
+              }
+            }
+          }
+          if (side) ev[6] += destroyed; else ev[5] += destroyed;
+          if (!isfinite(a0)) { X.rng.err |= LNW_ERRF_NAN_ROUND; COLW(c.radar_cur, a) = 0; }
+          else {
+            double rr = rint(a0);
+            COLW(c.radar_cur, a) = (int)fmin(fmax(rr, -2147483648.0), 2147483647.0);
+          }
+          uint32_t pn = COLW(c.pos_new, a);
+          moved = (pn & 0x80000000u) != 0;
+          if (moved) COLW(c.pos_cur, a) = pn & 0x7fffffffu;
         }
-        hits[side] += destroyed;
+        tp[0] += prof_now(S) - t0;
+        t0 = prof_now(S);
+        if (al && !(P.dbg_skip & 128)) {
+          if constexpr (REFW) march_pairs_ref(X, a);
+          if constexpr (ST) {
+            if (!side) get_obs_t<NB, NR, CW>(X, a, 0, NB);
+            else get_obs_t<NR, NB, CW>(X, a, NB, 0);
+          } else {
+            get_obs_dev(X, a);
+          }
+        }
+        tp[2] += prof_now(S) - t0;
+        t0 = prof_now(S);
+        double r = 0.0;
+        if (al && !(P.dbg_skip & 256)) r = reward_dev(X, a, moved, engage, destroyed);
+        COLW(c.reward, a) = r;
+        if (al) {
+          if (!side) {
+            if (P.side_blue ? destroyed > 0 : engage) COLB(c.eng, a) = 1;
+          } else {
+            if (!P.trained_red ? engage : destroyed > 1) COLB(c.eng, a) = 1;
+          }
+          hits[side] += destroyed;
+        }
+        tp[3] += prof_now(S) - t0;
+        if (emit) publish_progress(&prog, a + 1);
+        if (a < 8) prof_stamp(S, 6 + a);
       }
-      tp[3] += prof_now(S) - t0;
-      if (emit) publish_progress(&prog, a + 1);
-      if (a < 8) prof_stamp(S, 6 + a);
     }
     env_tail(P, S, c, lane, env, nb, A, N, ev, hits, nbp, nrp, bsx, bsy, rsx, rsy, X.rng, rew_b,
              rew_r, done_out, cog_out);
@@ -4112,7 +4394,8 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     const size_t uneed = (size_t)UNITS * ((step_lds_bytes(h) + 15) & ~(size_t)15);
     h->units_fit = uneed <= (size_t)UNITS_LDS_MAX;
     if (!(lds_opt_in & dbit) && (need > 64 * 1024 || gneed > 64 * 1024 || uneed > 64 * 1024)) {
-      const void *ks[16] = {(const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
+      const void *ks[17] = {(const void *)step_kernel<4, 4, true, false, 1, true>,
+                            (const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
                             (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
                             (const void *)step_kernel<2, 2, true>, (const void *)step_kernel<3, 3, true>,
                             (const void *)step_kernel<4, 4, true>, (const void *)step_kernel<0, 0, false, true>,
@@ -4257,7 +4540,14 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
         cog_dev);
   }
   else if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
-  else if (templated && h->nb == 4) { if (cw) LNW_STEP(4, 4, true, false); else LNW_STEP(4, 4, false, false); }
+  else if (templated && h->nb == 4) {
+    // the contact variant without rows: phase S split by side (step_kernel PS)
+    if (cw && k.no_obs && k.los_mode == 0 && !h->ana.eng_log && !h->ana.ew_log)
+      step_kernel<4, 4, true, false, 1, true><<<grid, dim3(2 * WAVE), lds, st>>>(
+          k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
+    else if (cw) LNW_STEP(4, 4, true, false);
+    else LNW_STEP(4, 4, false, false);
+  }
   else if (templated && h->nb == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }
   else if (templated && h->nb == 2) { if (cw) LNW_STEP(2, 2, true, false); else LNW_STEP(2, 2, false, false); }
   else if (use_group) {
