@@ -35,6 +35,20 @@ NAMES = {0: "small", 1: "large", 2: "ls"}
 @pytest.mark.parametrize("name", ["3v3_scripted", "4v2ls_trained", "4v4_trained_contact",
                                   "4v4_melee_done", "2v2_trained_breaks"])
 def test_rollout_matches_reference(name, impl):
+    _rollout_case(name, impl)
+
+
+@pytest.mark.parametrize("name", ["4v4_trained_contact", "4v4_melee_done"])
+def test_rollout_contact_variant_matches_reference(name):
+    """The contact variant's kernels on the same recorded rollouts, without a
+    per-step callback: the rollout's fast path (steps without rows, whose phase S
+    splits by side, and the two-wave observe), tape mode. The draw counters are
+    checked through every value the draws feed (a finished env's later draws
+    belong to no reference episode, so the final counter is not compared)."""
+    _rollout_case(name, "hip", contact=True)
+
+
+def _rollout_case(name, impl, contact=False):
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
     from lnw.rollout import BatchedActor, BatchedCritic, Rollout, gae
@@ -48,6 +62,8 @@ def test_rollout_matches_reference(name, impl):
                   tactics="aggressive", side="blue", auto_reset=False)
     g = BatchedGame(R, [NAMES[t] for t in types[:nb]], [NAMES[t] for t in types[nb:]],
                     scenario=sc, grid=grid, reward_dtype=torch.float64)
+    if contact:
+        g.set_variant(True)
     tapes = [fx["tape"][e["tape_start"]:e["tape_end"]] for e in eps]
     offs = np.concatenate([[0], np.cumsum([len(t) for t in tapes])]).astype(np.int64)
     g.set_tape(np.concatenate(tapes), offs)
@@ -70,7 +86,7 @@ def test_rollout_matches_reference(name, impl):
                 red_actor=red_actor, gamma=meta["gamma"], impl=impl)
     rng_after = []  # every env's draw counter after each step (the tape position)
     out = r.run(forced_actions=torch.from_numpy(fx["act"]).cuda(),
-                on_step=lambda t, o: rng_after.append(g.env_state()["rng"].copy()))
+                on_step=None if contact else (lambda t, o: rng_after.append(g.env_state()["rng"].copy())))
     torch.cuda.synchronize()
     run = out["running"].cpu().numpy()
     n_steps = np.array(meta["n_steps"])
@@ -103,6 +119,7 @@ def test_rollout_matches_reference(name, impl):
                                rtol=1e-5, atol=1e-5)
     # every env consumed exactly its episode's draws by the step that ended it
     # (draws a finished env makes afterwards belong to no reference episode)
-    used = np.array([rng_after[n - 1][e] for e, n in enumerate(n_steps)])
-    assert np.array_equal(used, [len(t) for t in tapes]), (used, [len(t) for t in tapes])
+    if not contact:
+        used = np.array([rng_after[n - 1][e] for e, n in enumerate(n_steps)])
+        assert np.array_equal(used, [len(t) for t in tapes]), (used, [len(t) for t in tapes])
     g.close()
