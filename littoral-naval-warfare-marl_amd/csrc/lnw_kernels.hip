@@ -2960,7 +2960,11 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   // rows leave during phase S from wave 1 (emit_wave_t) for full waves in LOS
   // table mode; the terrain mask LDS is then reused as the emission stage, so
   // the rare out-of-table LOS march reads the global copy
-  const bool emit = ST && P.los_mode != 1 && nenv == WAVE && !(P.dbg_skip & 3) && !P.no_obs;
+  // the contact variant's phase S split by side (step_kernel PS, below): its rows
+  // are written after phase S
+  const bool psplit = PS && CW && NB == 4 && NR == 4 && UN == 1 && EPW == WAVE && P.los_mode == 0 &&
+                      !(P.dbg_skip & 515) && !S.ana.eng_log && !S.ana.ew_log && !(P.dbg_skip & 16384);
+  const bool emit = ST && P.los_mode != 1 && nenv == WAVE && !(P.dbg_skip & 3) && !P.no_obs && !psplit;
   // two-wave workgroups share phases L and M (agents / pair passes split);
   // after M wave 1 turns to emission and wave 0 runs S
   constexpr int NW = ST && EPW == WAVE ? 2 : 1;
@@ -3044,25 +3048,20 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
       if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
     }
   }
-  // The contact variant without observation rows (lnw_step with NULL outputs:
-  // the MAPPO rollout's step) leaves wave 1 free after phase M. Phase S then
-  // splits by side (templated 4v4, loud workgroups): wave 0 plays blue's turns
-  // and wave 1 red's. Red's turns read blue only at its final cells and radars
-  // (known after phase M — the moves, and radar = rint(a0)), and
-  // blue's read red at its start cells and radars, so each wave works on its own
-  // view of the cells and radars (wave 1's copy: blue final, red at the start,
-  // in the emission stage's LDS, unused without rows). What ties the sides
-  // together is the draw counter: wave 1 counts blue's draws first — the fire
-  // loops' missile shots before a barrier (blue's get_obs then rewrites those
-  // lists), the get_obs walks' bearings after it — and starts red's turns past
-  // them. After a second barrier wave 0 merges red's hits, sums, counter and
-  // cells and runs the tail. (The engagement and EW-fix logs, whose records keep
-  // the turn order, keep phase S on wave 0.)
-  // (a separate instantiation, PS, so the contact variant's row-writing kernel
-  // keeps its code)
-  const bool psplit = PS && CW && NB == 4 && NR == 4 && UN == 1 && EPW == WAVE && P.no_obs &&
-                      P.los_mode == 0 && !(P.dbg_skip & 515) && !S.ana.eng_log && !S.ana.ew_log &&
-                      !(P.dbg_skip & 16384);
+  // The contact variant's phase S splits by side (templated 4v4, loud
+  // workgroups; step_kernel PS): wave 0 plays blue's turns and wave 1 red's, and
+  // the rows are written after it (phase O) instead of emitted by wave 1 during
+  // it. Red's turns read blue only at its final cells and radars (SURVEY §9 Q1:
+  // known after phase M — the moves, and radar = rint(a0)), and blue's read red
+  // at its start cells and radars, so each wave works on its own view of the
+  // cells and radars (wave 1's copy: blue final, red at the start, in the
+  // emission stage's LDS, unused without emission). What ties the sides together
+  // is the draw counter: wave 1 counts blue's draws first — the fire loops'
+  // missile shots before a barrier (blue's get_obs then rewrites those lists),
+  // the get_obs walks' bearings after it — and starts red's turns past them.
+  // After a second barrier wave 0 merges red's hits, sums, counter and cells and
+  // runs the tail. (The engagement and EW-fix logs, whose records keep the turn
+  // order, keep phase S on wave 0.)
   if (wid == 1 && !psplit) {
     if constexpr (ST) {
       if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
@@ -3862,6 +3861,7 @@ struct lnw_handle {
   int dbg_skip = 0;
   bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
   bool force_group = false;  // LNW_FORCE_GROUP (A/B): the group kernel for templated team sizes too
+  bool no_split_rows = false;  // LNW_NO_SPLIT_ROWS (A/B): row-writing contact steps keep phase S on one wave
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
@@ -4206,6 +4206,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
   h->force_group = getenv("LNW_FORCE_GROUP") != nullptr;
+  h->no_split_rows = getenv("LNW_NO_SPLIT_ROWS") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
   // LNW_NO_XCD_REMAP: workgroup b steps env chunk b (A/B tests of xcd_chunk)
@@ -4541,8 +4542,9 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   }
   else if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
   else if (templated && h->nb == 4) {
-    // the contact variant without rows: phase S split by side (step_kernel PS)
-    if (cw && k.no_obs && k.los_mode == 0 && !h->ana.eng_log && !h->ana.ew_log)
+    // the contact variant: phase S split by side (step_kernel PS; LNW_NO_SPLIT_ROWS:
+    // only for steps without rows, A/B)
+    if (cw && k.los_mode == 0 && !h->ana.eng_log && !h->ana.ew_log && (k.no_obs || !h->no_split_rows))
       step_kernel<4, 4, true, false, 1, true><<<grid, dim3(2 * WAVE), lds, st>>>(
           k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
     else if (cw) LNW_STEP(4, 4, true, false);
