@@ -2963,7 +2963,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   // the contact variant's phase S split by side (step_kernel PS, below): its rows
   // are written after phase S
   const bool psplit = PS && CW && NB == 4 && NR == 4 && UN == 1 && EPW == WAVE && P.los_mode == 0 &&
-                      !(P.dbg_skip & 515) && !S.ana.eng_log && !S.ana.ew_log && !(P.dbg_skip & 16384);
+                      !(P.dbg_skip & 515) && !(P.dbg_skip & 16384);
   const bool emit = ST && P.los_mode != 1 && nenv == WAVE && !(P.dbg_skip & 3) && !P.no_obs && !psplit;
   // two-wave workgroups share phases L and M (agents / pair passes split);
   // after M wave 1 turns to emission and wave 0 runs S
@@ -3060,8 +3060,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   // missile shots before a barrier (blue's get_obs then rewrites those lists),
   // the get_obs walks' bearings after it — and starts red's turns past them.
   // After a second barrier wave 0 merges red's hits, sums, counter and cells and
-  // runs the tail. (The engagement and EW-fix logs, whose records keep the turn
-  // order, keep phase S on wave 0.)
+  // runs the tail. (The analytics logs' records then interleave the two sides'
+  // turns; their order across envs is the atomics' order anyway.)
   if (wid == 1 && !psplit) {
     if constexpr (ST) {
       if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
@@ -3451,8 +3451,9 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
 // blue's walks alone (register bit arithmetic, no draws) to count them, starts
 // red's calls past them, and keeps its pooled-bearing tables in the actions'
 // LDS columns (unused here); the env's final counter and error bits are merged
-// after a barrier. (The EW-fix log, whose records keep the calls' order, and a
-// single side or ship keep the calls on wave 0.)
+// after a barrier. (A single side or ship keeps the calls on wave 0; the EW-fix
+// log's records then interleave the sides, their order across envs being the
+// atomics' order anyway.)
 template <int NB = 0, int NR = 0, bool CW = false>
 __global__ __launch_bounds__(NB > 0 && CW ? 2 * WAVE : WAVE) void observe_kernel(KParams P, KState S, int sel,
                                                                                  float *obs_b, float *obs_r) {
@@ -3481,7 +3482,7 @@ __global__ __launch_bounds__(NB > 0 && CW ? 2 * WAVE : WAVE) void observe_kernel
   if (sel >= 0) { a0 = sel; a1 = sel + 1; }
   else if (sel == LNW_OBS_BLUE) { a1 = nb; }
   else if (sel == LNW_OBS_RED) { a0 = nb; }
-  const bool split = NW > 1 && sel == LNW_OBS_ALL && !S.ana.ew_log;
+  const bool split = NW > 1 && sel == LNW_OBS_ALL;
   int wa0 = a0, wa1 = a1;  // this wave's calls
   if (NW > 1) {
     if (split) { wa0 = wid ? nb : 0; wa1 = wid ? A : nb; }
@@ -4544,7 +4545,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   else if (templated && h->nb == 4) {
     // the contact variant: phase S split by side (step_kernel PS; LNW_NO_SPLIT_ROWS:
     // only for steps without rows, A/B)
-    if (cw && k.los_mode == 0 && !h->ana.eng_log && !h->ana.ew_log && (k.no_obs || !h->no_split_rows))
+    if (cw && k.los_mode == 0 && (k.no_obs || !h->no_split_rows))
       step_kernel<4, 4, true, false, 1, true><<<grid, dim3(2 * WAVE), lds, st>>>(
           k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
     else if (cw) LNW_STEP(4, 4, true, false);
