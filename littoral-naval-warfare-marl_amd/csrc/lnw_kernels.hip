@@ -3056,10 +3056,9 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   // at its start cells and radars, so each wave works on its own view of the
   // cells and radars (wave 1's copy: blue final, red at the start, in the
   // emission stage's LDS, unused without emission). What ties the sides together
-  // is the draw counter: wave 1 counts blue's draws first — each blue ship's
-  // fire-loop missile shots before that ship's turn may start (its get_obs then
-  // rewrites the list; wave 0 waits on the progress counter), then the get_obs
-  // walks' bearings — and starts red's turns past them.
+  // is the draw counter: wave 1 counts blue's draws first — the fire loops'
+  // missile shots before a barrier (blue's get_obs then rewrites those lists),
+  // the get_obs walks' bearings after it — and starts red's turns past them.
   // After a second barrier wave 0 merges red's hits, sums, counter and cells and
   // runs the tail. (The analytics logs' records then interleave the two sides'
   // turns; their order across envs is the atomics' order anyway.)
@@ -3237,24 +3236,22 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
             COLW(cr.pos_cur, a) = p;
             COLW(cr.radar_cur, a) = r;
           }
-          // fire loops, each counted before blue's turn a may start (the turn's
-          // fire spends the missiles, its get_obs rewrites the list): wave 0
-          // waits on the progress counter (unused without emission)
-          for (int a = 0; a < NB; a++) {
-            if (COLB(c.alive0, a)) {
-              const double a1 = COLW(c.act1, a);
-              const int kind = COLB(c.akind, a);
-              const double engagement = P.discrete ? rint(a1) : a1;
-              const int keng = P.discrete ? K_PYINT : kind;
-              const int mk = COLB(c.mkind, a);
-              const double thr_v = kind_promote(keng, mk) == K_F32
-                                       ? (double)rintf((float)engagement * (float)COLB(c.miss_cur, a))
-                                       : rint(engagement * (double)COLB(c.miss_cur, a));
-              if (thr_v > 0.0 && COLW(c.tcnt, a) > 0 && !(P.dbg_skip & 65536))
-                nd += fire_draws(X, a, engagement, keng);
-            }
-            publish_progress(&prog, a + 1);
+          for (int a = 0; a < NB; a++) {  // fire loops, before blue's get_obs rewrites the lists
+            if (!COLB(c.alive0, a)) continue;
+            const double a1 = COLW(c.act1, a);
+            const int kind = COLB(c.akind, a);
+            const double engagement = P.discrete ? rint(a1) : a1;
+            const int keng = P.discrete ? K_PYINT : kind;
+            const int mk = COLB(c.mkind, a);
+            const double thr_v = kind_promote(keng, mk) == K_F32
+                                     ? (double)rintf((float)engagement * (float)COLB(c.miss_cur, a))
+                                     : rint(engagement * (double)COLB(c.miss_cur, a));
+            if (thr_v > 0.0 && COLW(c.tcnt, a) > 0 && !(P.dbg_skip & 65536))
+              nd += fire_draws(X, a, engagement, keng);
           }
+        }
+        __syncthreads();
+        if (wid == 1) {
 #pragma unroll
           for (int a = 0; a < NB; a++) {  // get_obs walks (their bearings), radar as take_action sets it
             if (!COLB(c.alive0, a)) continue;
@@ -3286,10 +3283,7 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
           COLW(cr.radar_cur, 1) = (int32_t)(uint32_t)(Y.rng.ctr >> 32);
           COLW(cr.radar_cur, 2) = (int32_t)Y.rng.err;
         } else {
-          for (int a = 0; a < NB; a++) {
-            wait_progress(&prog, a + 1);
-            turn(X, a, N, ev, hits, bsx, bsy, nbp, rsx, rsy, nrp, tp, t0);
-          }
+          for (int a = 0; a < NB; a++) turn(X, a, N, ev, hits, bsx, bsy, nbp, rsx, rsy, nrp, tp, t0);
         }
         __syncthreads();
         if (wid == 1) return;
