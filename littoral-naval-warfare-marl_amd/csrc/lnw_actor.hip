@@ -78,7 +78,7 @@ constexpr int CH_THREADS = 256;
 // pc: the thread's column of a [45][stride] LDS parking area for the pooled
 // conv1 maps.
 __device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pc, int stride,
-                                              bool running, float (&h)[12]) {
+                                              bool running, float (&h)[12], float *dump = nullptr) {
   // multiply-adds fused here (the build's -ffp-contract=off is for the step
   // kernels' bit-exactness; the policy is held to the tolerance of fp32 torch,
   // whose conv kernels fuse them too): half the VALU work of the head
@@ -92,6 +92,11 @@ __device__ __forceinline__ void conv_head_row(const float *P, const float *x, fl
   // a register before its load landed: tools/policy_determinism.py; the
   // strided policy input stays off for the same reason, rollout.py)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef LNW_PROBE_DUMP  // diagnostics only (tools/policy_determinism.py): the window as read
+  if (dump)
+#pragma unroll
+    for (int i = 0; i < WIN; i++) dump[i] = win[i];
+#endif
   // conv1 (1 -> 5, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (7x7 -> 3x3),
   // one channel at a time (rolled: 49 outputs live)
 #pragma unroll 1
@@ -442,10 +447,17 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
     float h[12];
 #ifdef LNW_PROBE_NOCONV  // timing probes only (tools/policy_probe.py): no conv head
     for (int k = 0; k < 12; k++) h[k] = x[k];
+#elif defined(LNW_PROBE_DUMP)  // diagnostics: window, LayerNorm output and heads per row
+    float *dbg = (float *)a.forced_act;
+    conv_head_row(P, x, warea + lane, WAVE, a.bn_running != 0, h, dbg + r * 64);
 #else
     conv_head_row(P, x, warea + lane, WAVE, a.bn_running != 0, h);
 #endif
     layer_norm_row<NI>(P, x, n_in, h, u);
+#ifdef LNW_PROBE_DUMP
+#pragma unroll
+    for (int k = 0; k < NI; k++) dbg[rows * 64 + r * NI + k] = u[k];
+#endif
   } else {
 #pragma unroll
     for (int k = 0; k < NI; k++) u[k] = 0.f;
@@ -527,6 +539,13 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
     }
     mean[v] = mv;
     lsd[v] = lv;
+  }
+#endif
+#ifdef LNW_PROBE_DUMP
+  if (valid) {
+    float *dh = (float *)a.forced_act + rows * (64 + NI) + r * 8;
+#pragma unroll
+    for (int v = 0; v < NOUT; v++) { dh[v] = mean[v]; dh[4 + v] = lsd[v]; }
   }
 #endif
   if (!valid) return;

@@ -113,6 +113,10 @@ __host__ __device__ inline int stage_bytes(int A, int nb, int nr, int G) {
 // (row stride EST4 float4s, odd: conflict-free ds_write_b128) | x/G LUT.
 constexpr int EST4 = 5;
 __host__ __device__ inline int estage_bytes(int G) { return WAVE * EST4 * 16 + ((G + 3) & ~3) * 4; }
+// wave 1's region in the phase-S split (step_kernel, psplit): pos and radar
+// copies (A padded columns each) and finish_obs_t's pooled-bearing tables
+// (rank -> lane bytes, rank -> draw u16s, fix table [nmax][WAVE] u32)
+__host__ __device__ constexpr int psplit_bytes(int A, int nmax) { return 2 * A * PAD * 4 + 3 * WAVE + 4 * WAVE * nmax; }
 
 // Quiet-path row stage: QEPG envs x one side's rows (stride stage_stride(ns)).
 constexpr int QEPG = 8;
@@ -162,7 +166,14 @@ __host__ __device__ inline LdsLayout lds_layout(int A, int nb, int nr, int nmax,
   L.mask = o;
   L.estage = o;
   // the emission stage exists only with full-wave workgroups (two-wave kernels)
-  const int est = EPW == WAVE ? estage_bytes(G) : 0;
+  int est = EPW == WAVE ? estage_bytes(G) : 0;
+  // the 4v4 phase-S split (psplit) keeps wave 1's pos / radar copies and its
+  // pooled-bearing tables here: 2 A PAD words + 3 WAVE + 4 WAVE nmax bytes
+  // (5 376 B at 4v4), which estage_bytes covers only from G = 64 on
+  if (EPW == WAVE && nb == 4 && nr == 4) {
+    const int ps = psplit_bytes(A, nmax);
+    if (est < ps) est = ps;
+  }
   o += mask_words * 4 > est ? mask_words * 4 : est;
   const int lut = ((G + 3) & ~3) * 4;
   if (o - L.qstage1 < qneed + lut) o = L.qstage1 + qneed + lut;
@@ -3216,7 +3227,8 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
       };
       if (psplit) {
         // wave 1's view: pos / radar copies and its pooled-bearing tables in the
-        // emission stage (2 x 2 080 + 1 216 B of its >= 5 520)
+        // emission stage (psplit_bytes: 2 x 2 080 + 1 216 B; lds_layout sizes
+        // the region to at least that for 4v4 whatever G is)
         Cols cr = c;
         cr.pos_cur = (uint32_t *)(lds_dyn + L.mask);
         cr.radar_cur = (int32_t *)(lds_dyn + L.mask + A * PAD * 4);
@@ -4432,22 +4444,20 @@ int lnw_set_rng(lnw_handle *h, int32_t mode, uint64_t seed, const double *tape_d
   return 0;
 }
 
-int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn,
-              const int32_t *pos_dev, void *stream) {
-  if (!h || !spawn) return fail(LNW_EINVAL, "null argument");
-  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
-  HIPCHK(hipSetDevice(h->device));
+// Validate a spawn spec's ship types (blue then red) and derive what the
+// kernels key on: each side's window cells (wc) and whether the runtime-size
+// kernels must run (has_medium). Shared by lnw_reset and lnw_set_state, so a
+// snapshot restored into any handle selects the same kernels and row lengths
+// as the handle it was taken from. apply = false only validates.
+static int apply_side_types(lnw_handle *h, const int32_t *types, bool apply) {
   int nmed[2] = {0, 0};
   for (int a = 0; a < h->A; a++) {
-    int t = spawn->types[a];
+    const int t = types[a];
     if (t != LNW_SMALL && t != LNW_LARGE && t != LNW_LS && t != LNW_MEDIUM)
       return fail(LNW_EUNSUPPORTED, "ship type must be small, large, ls or medium");
     if (t == LNW_MEDIUM) nmed[a >= h->nb]++;
     if (h->params.discrete && t == LNW_LS)
       return fail(LNW_EUNSUPPORTED, "LandingShip has no value_to_coordinates (DISCRETE mode)");
-    if (!spawn->rand_ls[a] && (spawn->pos[a][0] < 0 || spawn->pos[a][0] >= h->G ||
-                               spawn->pos[a][1] < 0 || spawn->pos[a][1] >= h->G))
-      return fail(LNW_EINVAL, "spawn position outside the grid");
   }
   // a side's row length follows its fastest ship (game.py:595-610), and a
   // medium ship's get_obs row has a 5x5 window (combatant.py:165-181): a side
@@ -4459,9 +4469,25 @@ int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn
       return fail(LNW_EUNSUPPORTED, "medium ships need a side of medium ships only (the reference's "
                                     "rows are sized by the fastest ship, game.py:595-610)");
   }
-  h->kp.wc[0] = nmed[0] ? 25 : 49;
-  h->kp.wc[1] = nmed[1] ? 25 : 49;
-  h->has_medium = nmed[0] || nmed[1];
+  if (apply) {
+    h->kp.wc[0] = nmed[0] ? 25 : 49;
+    h->kp.wc[1] = nmed[1] ? 25 : 49;
+    h->has_medium = nmed[0] || nmed[1];
+  }
+  return 0;
+}
+
+int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn,
+              const int32_t *pos_dev, void *stream) {
+  if (!h || !spawn) return fail(LNW_EINVAL, "null argument");
+  if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
+  HIPCHK(hipSetDevice(h->device));
+  if (int rc = apply_side_types(h, spawn->types, false)) return rc;
+  for (int a = 0; a < h->A; a++)
+    if (!spawn->rand_ls[a] && (spawn->pos[a][0] < 0 || spawn->pos[a][0] >= h->G ||
+                               spawn->pos[a][1] < 0 || spawn->pos[a][1] >= h->G))
+      return fail(LNW_EINVAL, "spawn position outside the grid");
+  apply_side_types(h, spawn->types, true);
   hipStream_t st = (hipStream_t)stream;
   HIPCHK(hipMemcpy(h->sp_types, spawn->types, sizeof(int32_t) * h->A, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->sp_pos, spawn->pos, sizeof(int32_t) * 2 * h->A, hipMemcpyHostToDevice));
@@ -4733,6 +4759,8 @@ int lnw_set_state(lnw_handle *h, const void *src, int64_t nbytes, void *stream) 
   HIPCHK(hipMemcpy(&hd, src, sizeof hd, hipMemcpyDefault));
   if (memcmp(hd.magic, "LNWSTATE", 8) != 0 || hd.version != 1)
     return fail(LNW_EINVAL, "not an lnw state snapshot (bad magic or version)");
+  if (hd.abi != LNW_ABI_VERSION)
+    return fail(LNW_EINVAL, "snapshot was taken by a library of another ABI version");
   const int64_t total = lnw_state_bytes(h);
   if (hd.E != h->E || hd.nb != h->nb || hd.nr != h->nr || hd.T != h->T || hd.G != h->G || hd.total != total)
     return fail(LNW_EINVAL, "snapshot shape (envs, team sizes, grid) differs from this handle");
@@ -4744,11 +4772,21 @@ int lnw_set_state(lnw_handle *h, const void *src, int64_t nbytes, void *stream) 
   std::vector<Section> s;
   if (int rc = state_sections(h, s)) return rc;
   const char *p = (const char *)src;
+  // the spawn types decide the kernels and the row lengths (wc, has_medium):
+  // validate them before anything is overwritten, apply them after
+  int32_t types[64];
+  {
+    int64_t ot = 256;
+    for (int i = 0; i < LNW_NFIELDS; i++) ot += sec_align(s[i].bytes);
+    HIPCHK(hipMemcpy(types, p + ot, sizeof types, hipMemcpyDefault));
+    if (int rc = apply_side_types(h, types, false)) return rc;
+  }
   int64_t o = 256;
   for (const Section &x : s) {
     if (x.dev) HIPCHK(hipMemcpy(x.dev, p + o, (size_t)x.bytes, hipMemcpyDefault));
     o += sec_align(x.bytes);
   }
+  apply_side_types(h, types, true);
   h->kp.rng_mode = hd.rng_mode;
   if (hd.rng_mode == LNW_RNG_PHILOX) h->kp.seed = hd.seed;
   for (int i = 0; i < 2; i++) { h->kp.box_lo[i] = hd.box_lo[i]; h->kp.box_hi[i] = hd.box_hi[i]; }

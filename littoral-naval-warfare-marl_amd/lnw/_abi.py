@@ -19,6 +19,7 @@ LNW_ERRF_ZERODIV, LNW_ERRF_NAN_ROUND, LNW_ERRF_TAPE, LNW_ERRF_MISSILES = 1, 2, 4
 
 (F_POS, F_RADAR, F_MISSILES, F_MKIND, F_ALIVE, F_TYPE, F_STEPS, F_DIST_LZ, F_TL_CNT, F_TL,
  F_DUCT, F_ENV, F_RNG, F_ERR) = range(14)
+LNW_NFIELDS = 14
 
 # exported symbols (must match include/lnw.h)
 SYMBOLS = [

@@ -364,6 +364,17 @@ class BatchedGame:
         saved handle would have. A tape-mode snapshot needs the same tape bound
         (set_tape) first."""
         buf = torch.as_tensor(snapshot, dtype=torch.uint8).contiguous()
+        # the observation buffers are sized by this game's ship types: a
+        # snapshot of another fleet (a medium side has shorter rows) is refused
+        # here, before the library would select kernels for its row length
+        off = 256
+        for f in range(_abi.LNW_NFIELDS):
+            off += (self._field(f)[1] + 255) & ~255
+        if buf.numel() >= off + 4 * self.A:
+            types = buf[off:off + 4 * self.A].cpu().view(torch.int32).tolist()
+            if types != [int(t) for t in self.blue_types + self.red_types]:
+                raise ValueError(f"snapshot fleet {types} differs from this game's "
+                                 f"{self.blue_types + self.red_types}")
         check(self.L.lnw_set_state(self.h, _ptr(buf), buf.numel(), self._stream()))
 
     def close(self):

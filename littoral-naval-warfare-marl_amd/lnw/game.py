@@ -88,6 +88,10 @@ class ShipProxy:
         self.n_actions = game.action_space
         self.n_obs = game.observation_space
         self.landing_zone = _LZ if ship_type == "ls" else None
+        # game.py:665 reads `landing_spot` (LandingShip stores the same cell as
+        # landing_zone, landingship.py:68; the reference's drawing of a red
+        # LandingShip would raise AttributeError there)
+        self.landing_spot = self.landing_zone
         self.replenishment_points = (game.blue_replenishment_points if side == "blue"
                                      else game.red_replenishment_points)
 
@@ -386,14 +390,25 @@ class Game:
             ax.set_aspect("equal")
             ax.imshow(np.asarray(self.grid), cmap="gray", origin="upper",
                       extent=[-0.5, 100 - 0.5, -0.5, 100 - 0.5])
-            marks = {"small": 4, "large": 8, "ls": 6}
+            # game.py:643-666: combatants as circles sized by type (small 4,
+            # medium 6, large 8); a red LandingShip as a square with its
+            # landing spot as a star (the reference draws no blue LandingShip)
+            marks = {"small": 4, "medium": 6, "large": 8}
             for col, ships in (("b", self.blue_ships), ("r", self.red_ships)):
                 for shp in ships:
                     if shp is None:
                         continue
                     x, y = shp.position
-                    ax.plot(y, 100 - x - 1, col + ("s" if shp.ship_type == "ls" else "o"),
-                            markersize=marks[shp.ship_type])
+                    if shp.ship_type in marks:
+                        ax.plot(y, 100 - x - 1, col + "o", markersize=marks[shp.ship_type])
+                    elif shp.ship_type == "ls" and col == "r":
+                        ax.plot(y, 100 - x - 1, "rs", markersize=6)
+                        lx, ly = shp.landing_spot
+                        ax.plot(ly, 100 - lx - 1, "r*", markersize=6)
+                for shp in ships:
+                    if shp is None:
+                        continue
+                    x, y = shp.position
                     if shp.radar_transmission == 1:
                         r = ((np.sqrt((4 / 3) * 6370 * 2) * (np.sqrt(shp.mast_height / 1000)
                                                              + np.sqrt(30 / 1000))) / 5

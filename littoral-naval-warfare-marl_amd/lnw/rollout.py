@@ -384,6 +384,11 @@ class Rollout:
         self.noise, self.bn, self.red_bn = noise, bn, red_bn
         self.gamma, self.stop_at_done, self.observe = float(gamma), stop_at_done, observe
         self.table = red_script_table(game.device) if red == "script" else None
+        # diagnostics / parity: keep each step's action array and row kinds as
+        # the policy wrote them (before the step's in-place salvo write-back)
+        # in the returned buffers ("step_actions" [E, T, A, 4] float64,
+        # "step_kinds" [E, T, A]); hip impl only
+        self.record_actions = False
         # rollout index of the keyed draws, on the device (advanced by run())
         self._call = torch.zeros(1, dtype=torch.int64, device=game.device)
 
@@ -438,6 +443,9 @@ class Rollout:
             fa = forced_actions.to(device=dev, dtype=torch.float32).contiguous()
             assert fa.shape == (E, T, A, 4)
         alive_p, _ = g._field(F_ALIVE)
+        if self.record_actions:
+            b["step_actions"] = torch.zeros((E, T, A, 4), dtype=torch.float64, device=dev)
+            b["step_kinds"] = torch.zeros((E, T, A), dtype=torch.uint8, device=dev)
         seed = int(self.keyed_seed if self.keyed_seed is not None else self.seed) & (2**64 - 1)
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         P = lambda t_: t_.data_ptr()  # noqa: E731
@@ -492,6 +500,9 @@ class Rollout:
                 ra.seed, ra.call_dev, ra.T, ra.t, ra.which = seed, P(self._call), T, t, 2
                 ra.row_base, ra.alive, ra.full = g.env_id_base * nr, alive_p, P(full)
                 _abi.check(L.lnw_policy_act(C.byref(ra), stream))
+            if self.record_actions:
+                b["step_actions"][:, t] = full
+                b["step_kinds"][:, t] = kinds
             out = g.step(full, kinds, obs=not direct)
             pp = RolloutPostArgs()
             pp.obs, pp.obs_env_stride, pp.E, pp.n, pp.D = pa.obs_out, T * nb * Db, E, nb, Db

@@ -1197,3 +1197,59 @@ void orc_fullsize_range(const orc_params *P, const uint8_t *grid, int G, int nb,
     }
     free(e); free(act); free(kinds); free(ob); free(orr);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Full-size rollout driver (tests/test_gpu_rollout_fullsize.py only): the  */
+/* env side of a MAPPO rollout (ppo.py:497-577) for the global envs [env0,  */
+/* env0 + n) of an E-env batch. Every step s: ship.get_obs() of every live  */
+/* ship, blue then red (their side effects: target lists, EW gauss draws),  */
+/* then Game.step on the action array acts[s][E][A][4] (doubles, row kinds  */
+/* kinds[s][E][A], as the device policy wrote them). Per (step, env): the   */
+/* 64-bit hash of the float32 blue observation rows (sum bits * mult mod    */
+/* 2^64, zero rows for sunk ships), the blue rewards (double) and done;     */
+/* auto-reset after done == 0 or `horizon` steps as the device does.       */
+/* ------------------------------------------------------------------------ */
+void orc_rollout_range(const orc_params *P, const uint8_t *grid, int G, int nb, int nr,
+                       const int *types, const int *pos, int pos_per_env, uint64_t seed, int64_t E,
+                       int64_t env0, int64_t n, int S, int horizon, const double *acts,
+                       const uint8_t *kinds_in, const uint64_t *mult, uint64_t *hash, double *rew,
+                       int32_t *done_out) {
+    int A = nb + nr, Db = 4 * nb + 52, Dr = 4 * nr + 52;
+    orc_env *e = (orc_env *)malloc(sizeof(orc_env));
+    double *act = (double *)malloc(sizeof(double) * 4 * A);
+    int *kinds = (int *)malloc(sizeof(int) * A);
+    double *row = (double *)malloc(sizeof(double) * (Db > Dr ? Db : Dr));
+    double *ob = (double *)malloc(sizeof(double) * nb * Db);
+    double *orr = (double *)malloc(sizeof(double) * nr * Dr);
+    double rb[ORC_MAX_AGENTS], rr[ORC_MAX_AGENTS], cog;
+    for (int64_t env = env0; env < env0 + n; env++) {
+        const int *p = pos_per_env ? pos + env * A * 2 : pos;
+        orc_env_init(e, P, grid, G, nb, nr);
+        orc_set_rng(e, 0, seed, (uint64_t)env, 0, NULL, 0, 0);
+        orc_reset(e, types, p, NULL);
+        for (int s = 0; s < S; s++) {
+            const int64_t se = (int64_t)s * E + env;
+            uint64_t h = 0;
+            for (int a = 0; a < A; a++) {
+                if (!e->s[a].alive) continue;
+                memset(row, 0, sizeof(double) * (Db > Dr ? Db : Dr));
+                get_obs(e, a, row);
+                if (a < nb)
+                    for (int q = 0; q < Db; q++) {
+                        float f = (float)row[q];
+                        uint32_t w;
+                        memcpy(&w, &f, 4);
+                        h += (uint64_t)w * mult[a * Db + q];
+                    }
+            }
+            hash[se] = h;
+            memcpy(act, acts + se * A * 4, sizeof(double) * 4 * A);
+            for (int a = 0; a < A; a++) kinds[a] = kinds_in[se * A + a];
+            int done = orc_step(e, act, kinds, ob, orr, rb, rr, &cog);
+            for (int a = 0; a < nb; a++) rew[se * nb + a] = rb[a];
+            done_out[se] = done;
+            if (done == 0 || e->steps_done >= horizon) orc_reset(e, types, p, NULL);
+        }
+    }
+    free(e); free(act); free(kinds); free(row); free(ob); free(orr);
+}

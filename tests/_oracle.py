@@ -72,6 +72,9 @@ def lib():
         L.orc_fullsize_range.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, P, C.c_int, P,
                                          C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                          C.c_int, P, P, P, P, P, P, P]
+        L.orc_rollout_range.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P, P, C.c_int,
+                                        C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                                        C.c_int, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -269,6 +272,42 @@ def fullsize(grid, nb, nr, types, pos, acts, mult, seed, horizon, *, pos_per_env
     if acts_after:
         return hsh, rew, done, cog, aft
     return hsh, rew, done, cog
+
+
+def rollout_env(grid, nb, nr, types, pos, acts, kinds, mult, seed, horizon, *, pos_per_env=False,
+                trained_red=False, threads=None):
+    """orc_rollout_range over all E envs: the env side of a MAPPO rollout
+    (ppo.py:497-577) on the action arrays a device rollout stepped, acts
+    [S, E, A, 4] float64 with row kinds [S, E, A]. Per (step, env): the hash of
+    the blue get_obs rows taken before the step (sum bits * mult mod 2^64, mult
+    over nb * (4 nb + 52) floats), the blue rewards [S, E, nb] (float64) and
+    done [S, E]."""
+    from concurrent.futures import ThreadPoolExecutor
+    L = lib()
+    S, E, A = acts.shape[:3]
+    grid = np.ascontiguousarray(grid, np.uint8)
+    acts = np.ascontiguousarray(acts, np.float64)
+    kinds = np.ascontiguousarray(kinds, np.uint8)
+    types = np.ascontiguousarray(types, np.int32)
+    pos = np.ascontiguousarray(pos, np.int32)
+    mult = np.ascontiguousarray(mult, np.uint64)
+    P = OrcParams(0, 0, 1, 1, int(trained_red), 0.4, 74, 70, 14, 82)
+    hsh = np.zeros((S, E), np.uint64)
+    rew = np.zeros((S, E, nb), np.float64)
+    done = np.zeros((S, E), np.int32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    chunk = (E + threads - 1) // threads
+
+    def run(i):
+        e0 = i * chunk
+        n = max(0, min(chunk, E - e0))
+        if n:
+            L.orc_rollout_range(C.byref(P), _p(grid), grid.shape[0], nb, nr, _p(types), _p(pos),
+                                int(pos_per_env), seed, E, e0, n, S, horizon, _p(acts), _p(kinds),
+                                _p(mult), _p(hsh), _p(rew), _p(done))
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, range(threads)))
+    return hsh, rew, done
 
 
 def load_fixture(name, golden_dir=GOLDEN):

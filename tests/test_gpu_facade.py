@@ -217,6 +217,30 @@ def test_facade_visualize_and_coa_path(tmp_path, monkeypatch):
     g.close()
 
 
+def test_facade_visualize_medium_fleet(tmp_path, monkeypatch):
+    """visualize_grid with a medium side (game.py:649-650, 659-660: medium
+    combatants drawn at marker size 6) and a red LandingShip with its landing
+    spot (game.py:663-666), after a few steps of main.py's test loop."""
+    monkeypatch.chdir(tmp_path)
+    from lnw.game import Game, ShipSpec
+    random.seed(6)
+    np.random.seed(6)
+    g = Game()
+    g.scenario.landing_ops, g.scenario.n_red_landingship = True, 1
+    blue = [ShipSpec("blue", "medium", p) for p in [(36, 50), (40, 52), (38, 47)]]
+    red = [ShipSpec("red", "large", p) for p in [(58, 55), (60, 60)]]
+    g.reset(3, 2, blue_ships=blue, red_ships=red)   # + the scenario's landing ship
+    assert [s.ship_type for s in g.blue_ships] == ["medium"] * 3
+    assert g.red_ships[-1].ship_type == "ls"
+    assert g.red_ships[-1].landing_spot == g.red_ships[-1].landing_zone
+    n = len(g.blue_ships) + len(g.red_ships)
+    for s in range(5):
+        g.step([np.random.random(4).astype(np.float32) for _ in range(n)])
+    g.visualize_grid(path=str(tmp_path))
+    assert g.imagen == 1 and (tmp_path / "imagen0.png").exists()
+    g.close()
+
+
 _LAUNCHED = """\
 import json, random, sys
 import numpy as np

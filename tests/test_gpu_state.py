@@ -21,6 +21,12 @@ CASES = {
     "8v10ls": dict(blue=["small"] * 8, red=["large"] * 8 + ["ls"] * 2, G=1, landing_ops=True,
                    trained_red=False, box_b=(30, 45, 90, 120), box_r=(45, 60, 95, 125), E=128,
                    dtype=torch.float64),
+    # a medium side (5x5 windows, 4n+28-float rows, runtime-size kernels):
+    # restored into a fresh handle that was never reset, the library must take
+    # the side's row length and kernels from the snapshot
+    "3v3medium": dict(blue=["medium"] * 3, red=["large"] * 3, G=0, landing_ops=False,
+                      trained_red=True, box_b=(30, 45, 40, 60), box_r=(50, 65, 45, 65), E=192,
+                      dtype=torch.float32),
 }
 
 
@@ -110,5 +116,20 @@ def test_snapshot_refuses_other_shapes_and_terrain():
     bad[0] ^= 0xFF
     with pytest.raises(_abi.LnwError, match="magic"):
         g.set_state(bad)
-    for x in (g, other, moved):
+    # another fleet of the same shape: its rows would not fit this game's buffers
+    med = _game(dict(cs, blue=["medium"] * 4), grids["grid100"], seed=1)
+    with pytest.raises(ValueError, match="fleet"):
+        med.set_state(snap)
+    # a snapshot whose side mixes medium and speed-3 ships is refused by the
+    # library before anything is overwritten
+    off = 256
+    for f in range(_abi.LNW_NFIELDS):
+        off += (g._field(f)[1] + 255) & ~255
+    mixed = snap.clone()
+    mixed[off:off + 4] = torch.tensor([_abi.LNW_MEDIUM], dtype=torch.int32).view(torch.uint8)
+    before = g.get_state()
+    with pytest.raises(_abi.LnwError, match="medium"):
+        _abi.check(g.L.lnw_set_state(g.h, mixed.data_ptr(), mixed.numel(), None))
+    assert torch.equal(g.get_state(), before)
+    for x in (g, other, moved, med):
         x.close()

@@ -1,10 +1,13 @@
-# Timing-probe builds of lnw_actor.hip alone (tools/policy_probe.py):
-# base, no conv head (LNW_PROBE_NOCONV), no MLP (LNW_PROBE_NOMLP)
+# Probe builds of lnw_actor.hip alone (tools/policy_probe.py timing,
+# tools/policy_determinism.py diagnostics): base, no conv head
+# (LNW_PROBE_NOCONV), no MLP (LNW_PROBE_NOMLP), per-stage dumps (LNW_PROBE_DUMP)
 set -e
 cd "$(dirname "$0")/.."
 C=littoral-naval-warfare-marl_amd/csrc
 F="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fPIC -shared -Iinclude -I$C"
+mkdir -p tools/probe
 /opt/rocm/bin/hipcc $F $C/lnw_actor.hip -o tools/probe/actor_base.so &
 /opt/rocm/bin/hipcc $F -DLNW_PROBE_NOCONV $C/lnw_actor.hip -o tools/probe/actor_NOCONV.so &
 /opt/rocm/bin/hipcc $F -DLNW_PROBE_NOMLP $C/lnw_actor.hip -o tools/probe/actor_NOMLP.so &
+/opt/rocm/bin/hipcc $F -DLNW_PROBE_DUMP $C/lnw_actor.hip -o tools/probe/actor_dump.so &
 wait

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Diagnostics: lnw_policy_act called repeatedly on the same rows (packed, and
 strided in place like the rollout's direct path) -- are the outputs
-bit-identical from call to call?  usage: python tools/policy_determinism.py [E] [reps]"""
+bit-identical from call to call?
+usage: python tools/policy_determinism.py [E] [reps] [variants,...]
+POLICY_LIB=path: an lnw_actor.hip-only build (tools/probe); with a build made
+with -DLNW_PROBE_DUMP, PROBE_DUMP=1 also compares the window each row read,
+its LayerNorm output and its heads, and checks the window against the input."""
 import ctypes as C
 import os
 import sys
@@ -21,9 +25,11 @@ def main():
         print("lib", path, flush=True)
     else:
         L = _abi.load()
+    dump = os.environ.get("PROBE_DUMP") == "1"
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     n, D, T, t = 4, 68, 40, 5
+    rows = E * n
     torch.manual_seed(0)
     actor = BatchedActor.for_obs(D).cuda()
     ap = actor.packed_policy()
@@ -34,12 +40,15 @@ def main():
     live = torch.ones(E, dtype=torch.bool, device="cuda")
     call = torch.zeros(1, dtype=torch.int64, device="cuda")
     out2 = torch.zeros((E, T, n, D), device="cuda")
+    dbg = torch.zeros(rows * (64 + 32 + 8), device="cuda") if dump else None
     variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["packed", "strided", "strided_sync",
-                                                                   "strided_copy", "packed_inplace"]
+                                                                   "strided_copy", "packed_inplace",
+                                                                   "strided_nolive", "strided_noout"]
     for var in variants:
         strided = var.startswith("strided")
         ref = None
         nd = 0
+        waves = set()
         for k in range(reps):
             buf[:, t] = obs
             if var == "strided_sync":
@@ -62,22 +71,44 @@ def main():
                 pa.live = None
             if var == "strided_noout":
                 pa.obs_out = None
+            if dump:
+                dbg.zero_()
+                pa.forced_act = dbg.data_ptr()
             pa.act_out, pa.logp_out, pa.act_env_stride = acts.data_ptr() + t * n * 16, logp.data_ptr() + t * n * 16, T * n * 4
             pa.full = full.data_ptr()
             assert L.lnw_policy_act(C.byref(pa), None) == 0
             torch.cuda.synchronize()
-            cur = (acts[:, t].clone(), logp[:, t].clone(), full.clone())
+            cur = [acts[:, t].clone(), logp[:, t].clone(), full.clone()]
+            names = ["act", "logp", "full"]
+            if dump:
+                win = dbg[:rows * 64].view(rows, 64)[:, :49].clone()
+                bad_in = (win != obs.reshape(rows, D)[:, :49]).any(1)
+                if bool(bad_in.any()):
+                    idx = bad_in.nonzero().flatten()
+                    print(var, "rep", k, "window != input in", int(idx.numel()), "rows, waves",
+                          sorted(set((idx // 64).tolist()))[:8], flush=True)
+                cur += [win, dbg[rows * 64:rows * 96].view(rows, 32).clone(),
+                        dbg[rows * 96:].view(rows, 8).clone()]
+                names += ["window", "layernorm", "heads"]
             if ref is None:
                 ref = cur
                 continue
-            for name, x, y in zip(("act", "logp", "full"), cur, ref):
+            for name, x, y in zip(names, cur, ref):
                 if not torch.equal(x, y):
                     d = (x != y).nonzero()
                     nd += 1
-                    if nd <= 3:
-                        print(var, "rep", k, name, int((x != y).sum()), "differ, e.g.", d[0].tolist(),
-                              float(x[tuple(d[0])]), float(y[tuple(d[0])]), flush=True)
-        print(var, "mismatching (rep, output) pairs:", nd, "of", 3 * (reps - 1), flush=True)
+                    rr = d[:, 0] * (n if name in ("act", "logp") else 1)
+                    if name in ("act", "logp"):
+                        rr = d[:, 0] * n + d[:, 1]
+                    if name == "full":
+                        rr = d[:, 0] * n + d[:, 1]
+                    waves |= set((rr // 64).tolist())
+                    if nd <= 6:
+                        print(var, "rep", k, name, int((x != y).sum()), "differ, max |d|",
+                              float((x - y).abs().max()), "rows", sorted(set(rr.tolist()))[:6],
+                              "waves", sorted(set((rr // 64).tolist()))[:6], flush=True)
+        print(var, "mismatching (rep, output) pairs:", nd, "of", len(ref) * (reps - 1),
+              "waves involved:", len(waves), sorted(waves)[:10], flush=True)
 
 
 if __name__ == "__main__":
