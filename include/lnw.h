@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define LNW_ABI_VERSION 4
+#define LNW_ABI_VERSION 5
 
 /* status codes */
 #define LNW_OK 0
@@ -167,6 +167,26 @@ int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn
 int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
              float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
              int32_t *done_dev, float *cog_dev, void *stream);
+
+/* K consecutive Game.step calls whose action arrays the caller has ahead of
+ * time (an open-loop action sequence: scripted or replayed agents, benchmark
+ * actions) — no reference counterpart beyond K calls of Game.step; results are
+ * exactly those of K lnw_step calls, step k reading actions_dev + k *
+ * seq->act_step elements (and row kinds + k * kind_step bytes) and writing its
+ * outputs at the output pointers + k * the output strides (elements; a stride
+ * 0 makes every step write the same rows, each step's outputs replacing the
+ * previous step's as K separate calls would). For the templated 4v4 default
+ * variant the K steps run in one launch and each workgroup moves through them
+ * on its own, so one CU's step head overlaps another's observation stream;
+ * other shapes run K lnw_step launches. */
+typedef struct lnw_seq {
+  int32_t steps;               /* K >= 1 */
+  int64_t act_step, kind_step; /* action elements / row-kind bytes between steps */
+  int64_t obs_blue_step, obs_red_step, rew_blue_step, rew_red_step, done_step, cog_step;
+} lnw_seq;
+int lnw_step_seq(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t action_dtype,
+                 const uint8_t *row_kind_dev, float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev,
+                 float *rew_red_dev, int32_t *done_dev, float *cog_dev, void *stream);
 
 /* agent >= 0: that agent (blue 0..nb-1, red nb..A-1) in every env;
  * LNW_OBS_ALL / LNW_OBS_BLUE / LNW_OBS_RED: every live ship of the selection,

@@ -71,32 +71,23 @@ __device__ inline void bn_relu(float (&v)[N], const float *w, const float *b, co
 }
 
 constexpr int CH_THREADS = 256;
+// lnw_policy_act's block (probe builds may change it: tools/build_probes.sh)
+#ifndef LNW_PA_THREADS
+#define LNW_PA_THREADS 512
+#endif
+constexpr int PA_THREADS = LNW_PA_THREADS;
 
 // The conv head of one row (network.py:70-82): conv 1->5 over the 7x7 window
-// x[0..48] -> BN -> ReLU -> 2x2 pool, conv 5->8 -> BN -> ReLU -> pool, folded
-// into the linear 8->12 (h). P: packed parameters in LDS (broadcast reads);
-// pc: the thread's column of a [45][stride] LDS parking area for the pooled
-// conv1 maps.
-__device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pc, int stride,
-                                              bool running, float (&h)[12], float *dump = nullptr) {
+// win[0..48] (registers) -> BN -> ReLU -> 2x2 pool, conv 5->8 -> BN -> ReLU ->
+// pool, folded into the linear 8->12 (h). P: packed parameters in LDS
+// (broadcast reads); pc: the thread's column of a [45][stride] LDS parking area
+// for the pooled conv1 maps.
+__device__ __forceinline__ void conv_head_win(const float *P, const float (&win)[WIN], float *pc, int stride,
+                                              bool running, float (&h)[12]) {
   // multiply-adds fused here (the build's -ffp-contract=off is for the step
   // kernels' bit-exactness; the policy is held to the tolerance of fp32 torch,
   // whose conv kernels fuse them too): half the VALU work of the head
 #pragma clang fp contract(fast)
-  float win[WIN];
-#pragma unroll
-  for (int i = 0; i < WIN; i++) win[i] = x[i];
-  // every load of the row done before any use: around these loads the
-  // compiler spills registers to scratch and its partial vmcnt waits then do
-  // not hold (a row spread over distant lines, e.g. in a rollout buffer, read
-  // a register before its load landed: tools/policy_determinism.py; the
-  // strided policy input stays off for the same reason, rollout.py)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef LNW_PROBE_DUMP  // diagnostics only (tools/policy_determinism.py): the window as read
-  if (dump)
-#pragma unroll
-    for (int i = 0; i < WIN; i++) dump[i] = win[i];
-#endif
   // conv1 (1 -> 5, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (7x7 -> 3x3),
   // one channel at a time (rolled: 49 outputs live)
 #pragma unroll 1
@@ -129,52 +120,66 @@ __device__ __forceinline__ void conv_head_row(const float *P, const float *x, fl
       }
   }
   // conv2 (5 -> 8, 3x3, pad 1) -> BN -> ReLU -> 2x2 max pool (3x3 -> 1x1),
-  // folded straight into the linear 8 -> 12 (convhead). All 8 output maps
-  // accumulate together while the input channels stream in from LDS one at a
-  // time (9 inputs live instead of 45).
-  float v2[8][9];
-#pragma unroll
-  for (int co = 0; co < 8; co++)
-#pragma unroll
-    for (int p = 0; p < 9; p++) v2[co][p] = P[C2B + co];
-#pragma unroll 1
-  for (int ci = 0; ci < 5; ci++) {
-    float pin[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) pin[k] = pc[(ci * 9 + k) * stride];
-#pragma unroll
-    for (int co = 0; co < 8; co++) {
-      const float *w = P + C2W + (co * 5 + ci) * 9;
-#pragma unroll
-      for (int i = 0; i < 3; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-#pragma unroll
-          for (int ki = 0; ki < 3; ki++)
-#pragma unroll
-            for (int kj = 0; kj < 3; kj++) {
-              const int ii = i + ki - 1, jj = j + kj - 1;
-              if (ii >= 0 && ii < 3 && jj >= 0 && jj < 3) v2[co][i * 3 + j] += w[ki * 3 + kj] * pin[ii * 3 + jj];
-            }
-    }
-  }
+  // folded straight into the linear 8 -> 12 (convhead). Four output maps at a
+  // time accumulate while the input channels stream in from LDS one at a time
+  // (36 accumulators and 9 inputs live: the head then fits the kernel's
+  // registers without spilling; h sums the maps in the same order).
 #pragma unroll
   for (int k = 0; k < 12; k++) h[k] = P[HB + k];
+#pragma unroll 1
+  for (int c0 = 0; c0 < 8; c0 += 4) {
+    float v2[4][9];
 #pragma unroll
-  for (int co = 0; co < 8; co++) {
-    bn_relu<9>(v2[co], P + B2W, P + B2B, P + B2M, P + B2V, co, running);
-    const float f = fmaxf(fmaxf(v2[co][0], v2[co][1]), fmaxf(v2[co][3], v2[co][4]));
+    for (int co = 0; co < 4; co++)
 #pragma unroll
-    for (int k = 0; k < 12; k++) h[k] += P[HW + k * 8 + co] * f;
+      for (int p = 0; p < 9; p++) v2[co][p] = P[C2B + c0 + co];
+#pragma unroll 1
+    for (int ci = 0; ci < 5; ci++) {
+      float pin[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) pin[k] = pc[(ci * 9 + k) * stride];
+#pragma unroll
+      for (int co = 0; co < 4; co++) {
+        const float *w = P + C2W + ((c0 + co) * 5 + ci) * 9;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int ki = 0; ki < 3; ki++)
+#pragma unroll
+              for (int kj = 0; kj < 3; kj++) {
+                const int ii = i + ki - 1, jj = j + kj - 1;
+                if (ii >= 0 && ii < 3 && jj >= 0 && jj < 3) v2[co][i * 3 + j] += w[ki * 3 + kj] * pin[ii * 3 + jj];
+              }
+      }
+    }
+#pragma unroll
+    for (int co = 0; co < 4; co++) {
+      bn_relu<9>(v2[co], P + B2W, P + B2B, P + B2M, P + B2V, c0 + co, running);
+      const float f = fmaxf(fmaxf(v2[co][0], v2[co][1]), fmaxf(v2[co][3], v2[co][4]));
+#pragma unroll
+      for (int k = 0; k < 12; k++) h[k] += P[HW + k * 8 + c0 + co] * f;
+    }
   }
 }
 
-// LayerNorm over [h, x[49:]] (biased variance) with its affine, into u[0..n_in)
-template <int NI>
-__device__ __forceinline__ void layer_norm_row(const float *P, const float *x, int n_in, const float (&h)[12],
-                                               float (&u)[NI]) {
+// conv_head_win on a row in memory (features_kernel)
+__device__ __forceinline__ void conv_head_row(const float *P, const float *x, float *pc, int stride,
+                                              bool running, float (&h)[12]) {
+  float win[WIN];
 #pragma unroll
-  for (int k = 0; k < NI; k++) u[k] = k < 12 ? h[k < 12 ? k : 0] : (k < n_in ? x[WIN + k - 12] : 0.f);
+  for (int i = 0; i < WIN; i++) win[i] = x[i];
+  conv_head_win(P, win, pc, stride, running, h);
+}
+
+// LayerNorm over [h, tail] (biased variance; tail = x[49:], n_in - 12 values)
+// with its affine, into u[0..n_in)
+template <int NI>
+__device__ __forceinline__ void layer_norm_tail(const float *P, const float (&tl)[NI - 12], int n_in,
+                                                const float (&h)[12], float (&u)[NI]) {
+#pragma unroll
+  for (int k = 0; k < NI; k++) u[k] = k < 12 ? h[k < 12 ? k : 0] : (k < n_in ? tl[k < 12 ? 0 : k - 12] : 0.f);
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NI; k++) s += k < n_in ? u[k] : 0.f;
@@ -188,27 +193,40 @@ __device__ __forceinline__ void layer_norm_row(const float *P, const float *x, i
   for (int k = 0; k < NI; k++) u[k] = k < n_in ? (u[k] - mean) * inv * lw[k] + lb[k] : 0.f;
 }
 
-__global__ __launch_bounds__(CH_THREADS, 2) void features_kernel(const float *params, int obs_dim,
-                                                              const float *obs, long long B,
-                                                              int bn_running, float *out) {
+// the LayerNorm tail of a row in memory: x[49 .. D - 1], every load issued at
+// once (indices clamped into the row, values past n_in - 12 unused)
+template <int NT>
+__device__ __forceinline__ void load_tail(const float *x, int D, float (&tl)[NT]) {
+#pragma unroll
+  for (int k = 0; k < NT; k++) tl[k] = x[WIN + k < D ? WIN + k : D - 1];
+}
+
+// (the torch implementation's conv head, off the fused path: one wave per
+// SIMD, so the compiler has the registers to keep the head out of scratch)
+template <int NI>
+__global__ __launch_bounds__(CH_THREADS, 1) void features_kernel(const float *params, int obs_dim,
+                                                              const float *obs, int B, int bn_running,
+                                                              float *out) {
   const int n_in = obs_dim - WIN + 12;
   const int n_par = CONV_PARAMS + 2 * n_in;
   float *P = actor_lds;                           // [n_par] parameters
-  float *pool1 = actor_lds + n_par;               // [45][CH_THREADS] pooled conv1 maps
+  // pooled conv1 maps: per wave [45][64], one column per lane (as lnw_policy_act)
+  float *pool1 = actor_lds + n_par + (threadIdx.x / WAVE) * 45 * WAVE + (threadIdx.x & (WAVE - 1));
   for (int i = threadIdx.x; i < n_par; i += blockDim.x) P[i] = params[i];
   __syncthreads();
   const bool running = bn_running != 0;
-  const int t = threadIdx.x;
-  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < B;
-       row += (long long)gridDim.x * blockDim.x) {
-    const float *x = obs + row * obs_dim;
+  // (one row per thread, 32-bit row indices checked on the host; the tail is
+  // loaded after the head: nothing but the row index lives across it)
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row < B) {
     float h[12];
-    conv_head_row(P, x, pool1 + t, CH_THREADS, running, h);
-    float u[MAX_IN];
-    layer_norm_row<MAX_IN>(P, x, n_in, h, u);
-    float *o = out + row * n_in;
+    conv_head_row(P, obs + (long long)row * obs_dim, pool1, WAVE, running, h);
+    float tl[NI - 12], u[NI];
+    load_tail(obs + (long long)row * obs_dim, obs_dim, tl);
+    layer_norm_tail<NI>(P, tl, n_in, h, u);
+    float *o = out + (long long)row * n_in;
 #pragma unroll
-    for (int k = 0; k < MAX_IN; k++)
+    for (int k = 0; k < NI; k++)
       if (k < n_in) o[k] = u[k];
   }
 }
@@ -394,70 +412,88 @@ __device__ __forceinline__ void tanh_all(f32x4v (&acc)[4][NTO]) {
       for (int v = 0; v < 4; v++) acc[rt][nt][v] = tanh_fast(acc[rt][nt][v]);
 }
 
-template <int NI>
-__global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa) {
-  constexpr int Q1 = NI / 16;        // fc1 k-quads (n_in zero-padded to NI)
-  constexpr int KS = NI + 4;         // row stride of the wave's fc1 input tile (16-B aligned)
+// fc1 / fc2 / fc3 and both heads of the wave's 64 rows on the matrix cores
+// (xb: fc1's B operand), then each row's head outputs brought to its own lane
+template <int Q1>
+__device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const float *xt, int lane, int g, int m,
+                                          float (&mean)[NOUT], float (&lsd)[NOUT]) {
+  constexpr int KS = 16 * Q1 + 4;  // the tile's row stride (policy_act_kernel)
   const lnw_policy_args &a = pa.a;
-  const int n_in = pa.n_in;
-  const int n_par = CONV_PARAMS + 2 * n_in;
-  float *P = actor_lds;                // [n_par] conv head + LayerNorm parameters
-  // per wave: [45][64] pooled conv1 maps (one column per lane), then the
-  // wave's fc1 input tile [64][KS] over the same floats
-  constexpr int WAREA = (45 > KS ? 45 : KS) * WAVE;
-  float *warea = actor_lds + ((n_par + 3) & ~3) + (threadIdx.x / WAVE) * WAREA;
-  for (int i = threadIdx.x; i < n_par; i += blockDim.x) P[i] = a.params[i];
-  const int n = a.n, D = a.D;
-  const long long rows = a.E * n;
-  const long long r0 = (long long)blockIdx.x * CH_THREADS;
-  const long long istride = a.obs_in_env_stride ? a.obs_in_env_stride : (long long)n * D;
-  __syncthreads();
-  const int lane = threadIdx.x & (WAVE - 1), g = lane >> 4, m = lane & 15;
-  const long long r = r0 + threadIdx.x;
-  const bool valid = r < rows;  // (every lane stays for the wave-wide MFMAs)
-  const long long e = valid ? r / n : 0;
-  const int i = valid ? (int)(r - e * n) : 0;
-  const long long E = a.E;
-  const bool alive = valid && a.alive[(long long)(a.own0 + i) * E + e] != 0;
-  const bool live = !a.live || (valid && a.live[e] != 0);
-  // ---- env-level side work by the lane of ship 0 ---------------------------
-  if (valid && i == 0) {
-    if (a.script) {  // scripted rows: profile j for red ship j < script_n, zeros past the table
-      for (int j = 0; j < a.script_cnt; j++) {
-        const int ag = a.script_own0 + j;
-        const bool al = a.alive[(long long)ag * E + e] != 0;
-        const bool has = j < a.script_n && a.t < a.script_steps;
-        f64x4 v = {0.0, 0.0, 0.0, 0.0};
-        if (al && has) v = *(const f64x4 *)(a.script + ((long long)j * a.script_steps + a.t) * 4);
-        *(f64x4 *)(a.full + (e * a.A + ag) * 4) = v;
-      }
+  f32x4v xb[4][Q1];
+#pragma unroll
+  for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+    for (int q = 0; q < Q1; q++) xb[rt][q] = *(const f32x4v *)(xt + (rt * 16 + m) * KS + 16 * q + 4 * g);
+  // weights: three bf16 planes per layer (mfma_layer3), layers in order
+  const bf16x8 *Fw = (const bf16x8 *)(a.params + pa.off_w1);
+  constexpr int O2 = 3 * 4 * (Q1 / 2) * WAVE, O3 = O2 + 3 * 4 * 2 * WAVE, OH = O3 + 3 * 2 * 2 * WAVE;
+  const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
+  f32x4v h1[4][4];
+  bias_init<4>(bias, h1, g);
+  mfma_layer3<4, Q1>(Fw, xb, h1, lane);
+  tanh_all<4>(h1);
+  f32x4v h2[4][4];
+  bias_init<4>(bias + 64, h2, g);
+  mfma_layer3<4, 4>(Fw + O2, h1, h2, lane);
+  tanh_all<4>(h2);
+  f32x4v h3[4][2];
+  bias_init<2>(bias + 128, h3, g);
+  mfma_layer3<2, 4>(Fw + O3, h2, h3, lane);
+  tanh_all<2>(h3);
+  f32x4v hh[4][1];
+#pragma unroll
+  for (int rt = 0; rt < 4; rt++) hh[rt][0] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  mfma_layer3<1, 2>(Fw + OH, h3, hh, lane);
+  // head outputs of row 16 rt + m sit in lane m (normal head, n = v) and lane
+  // 16 + m (log-std head, n = 4 + v) of tile rt: bring row `lane` to lane
+  // `lane` (rt = g) for the per-row sampling below
+#pragma unroll
+  for (int v = 0; v < NOUT; v++) {
+    float mv = 0.f, lv = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) {
+      const float sm = __shfl(hh[rt][0][v], m);
+      const float sl = __shfl(hh[rt][0][v], 16 + m);
+      mv = g == rt ? sm : mv;
+      lv = g == rt ? sl : lv;
     }
-    if (a.kinds) {
-      bool all = true;
-      for (int ag = 0; ag < a.A; ag++) all = all && a.alive[(long long)ag * E + e] != 0;
-      const uint8_t k = (a.kinds_f32_all_alive && all) ? (uint8_t)LNW_KIND_F32 : (uint8_t)LNW_KIND_F64;
-      for (int ag = 0; ag < a.A; ag++) a.kinds[e * a.A + ag] = k;
-      if (a.f32_out) a.f32_out[e * a.f32_env_stride] = k == LNW_KIND_F32 ? 1 : 0;
-    }
+    mean[v] = mv;
+    lsd[v] = lv;
   }
+}
+
+// A wave's rows up to the fc1 tile: conv head + LayerNorm (one row per lane),
+// the observation copy for the rollout buffer, and the LayerNorm outputs into
+// the wave's fc1 input tile in LDS (xt) for mlp_heads.
+template <int NI>
+__device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *P, float *warea, int lane,
+                                             bool valid, long long e, int i, long long istride, long long r0,
+                                             long long rows) {
+  constexpr int KS = NI + 4;
+  const lnw_policy_args &a = pa.a;
+  const int n = a.n, D = a.D, n_in = pa.n_in;
   // ---- conv head + LayerNorm, one row per lane -------------------------------
+  // The row's window and LayerNorm tail are loaded once, every load issued
+  // together, into registers (the tail's loads were one dependent round trip
+  // each behind the k < n_in guard).
   float u[NI];
   if (valid) {
-    const float *x = a.obs + e * istride + (long long)i * D;
     float h[12];
-#ifdef LNW_PROBE_NOCONV  // timing probes only (tools/policy_probe.py): no conv head
-    for (int k = 0; k < 12; k++) h[k] = x[k];
-#elif defined(LNW_PROBE_DUMP)  // diagnostics: window, LayerNorm output and heads per row
-    float *dbg = (float *)a.forced_act;
-    conv_head_row(P, x, warea + lane, WAVE, a.bn_running != 0, h, dbg + r * 64);
-#else
-    conv_head_row(P, x, warea + lane, WAVE, a.bn_running != 0, h);
-#endif
-    layer_norm_row<NI>(P, x, n_in, h, u);
-#ifdef LNW_PROBE_DUMP
+    {
+      const float *x = a.obs + e * istride + (long long)i * D;
+      float win[WIN];
 #pragma unroll
-    for (int k = 0; k < NI; k++) dbg[rows * 64 + r * NI + k] = u[k];
+      for (int k = 0; k < WIN; k++) win[k] = x[k];
+#ifdef LNW_PROBE_NOCONV  // timing probes only (tools/policy_probe.py): no conv head
+      for (int k = 0; k < 12; k++) h[k] = win[k];
+#else
+      conv_head_win(P, win, warea + lane, WAVE, a.bn_running != 0, h);
 #endif
+    }
+    // the tail after the head (its registers are the head's), one batch of loads
+    float tl[NI - 12];
+    load_tail(a.obs + e * istride + (long long)i * D, D, tl);
+    layer_norm_tail<NI>(P, tl, n_in, h, u);
   } else {
 #pragma unroll
     for (int k = 0; k < NI; k++) u[k] = 0.f;
@@ -493,62 +529,181 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   for (int k4 = 0; k4 < NI / 4; k4++)
     *(f32x4v *)(xt + lane * KS + 4 * k4) = f32x4v{u[4 * k4], u[4 * k4 + 1], u[4 * k4 + 2], u[4 * k4 + 3]};
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  f32x4v xb[4][Q1];
-#pragma unroll
-  for (int rt = 0; rt < 4; rt++)
-#pragma unroll
-    for (int q = 0; q < Q1; q++) xb[rt][q] = *(const f32x4v *)(xt + (rt * 16 + m) * KS + 16 * q + 4 * g);
-  // ---- MLP on the matrix cores ----------------------------------------------
-#ifdef LNW_PROBE_NOMLP  // timing probes only: no MLP
-  float mean[NOUT], lsd[NOUT];
-  for (int v = 0; v < NOUT; v++) { mean[v] = xb[0][0][v]; lsd[v] = 0.f; }
-#else
-  // weights: three bf16 planes per layer (mfma_layer3), layers in order
-  const bf16x8 *Fw = (const bf16x8 *)(a.params + pa.off_w1);
-  constexpr int O2 = 3 * 4 * (Q1 / 2) * WAVE, O3 = O2 + 3 * 4 * 2 * WAVE, OH = O3 + 3 * 2 * 2 * WAVE;
-  const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
-  f32x4v h1[4][4];
-  bias_init<4>(bias, h1, g);
-  mfma_layer3<4, Q1>(Fw, xb, h1, lane);
-  tanh_all<4>(h1);
-  f32x4v h2[4][4];
-  bias_init<4>(bias + 64, h2, g);
-  mfma_layer3<4, 4>(Fw + O2, h1, h2, lane);
-  tanh_all<4>(h2);
-  f32x4v h3[4][2];
-  bias_init<2>(bias + 128, h3, g);
-  mfma_layer3<2, 4>(Fw + O3, h2, h3, lane);
-  tanh_all<2>(h3);
-  f32x4v hh[4][1];
-#pragma unroll
-  for (int rt = 0; rt < 4; rt++) hh[rt][0] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  mfma_layer3<1, 2>(Fw + OH, h3, hh, lane);
-  // head outputs of row 16 rt + m sit in lane m (normal head, n = v) and lane
-  // 16 + m (log-std head, n = 4 + v) of tile rt: bring row `lane` to lane
-  // `lane` (rt = g) for the per-row sampling below
-  float mean[NOUT], lsd[NOUT];
-#pragma unroll
-  for (int v = 0; v < NOUT; v++) {
-    float mv = 0.f, lv = 0.f;
-#pragma unroll
-    for (int rt = 0; rt < 4; rt++) {
-      const float sm = __shfl(hh[rt][0][v], m);
-      const float sl = __shfl(hh[rt][0][v], 16 + m);
-      mv = g == rt ? sm : mv;
-      lv = g == rt ? sl : lv;
+}
+
+#ifdef LNW_PROBE_DISTURB
+// Diagnostics probes only: what the other wave of a SIMD does while a wave
+// runs its MLP (1 VALU FMA chains, 2 LDS reads of its own tile, 3 global
+// loads, 4 s_sleep, 5 MFMA chains on registers, 6 LDS writes past its tile,
+// 7 global stores to its rows' log-prob outputs (rewritten after), 8 v_exp /
+// v_log / v_rcp / v_sqrt chains, 9 integer hashing); nothing it computes is kept.
+template <int MODE, int KS>
+__device__ __noinline__ void disturb(const PolicyArgs &pa, float *warea, int lane, long long e, int i) {
+  float acc0 = (float)lane, acc1 = 1.f, acc2 = 2.f, acc3 = 3.f;
+  if (MODE == 1) {
+    for (int it = 0; it < 2000; it++) {
+      acc0 = fmaf(acc0, 1.0001f, 0.5f); acc1 = fmaf(acc1, 0.9999f, 0.25f);
+      acc2 = fmaf(acc2, 1.0002f, 0.125f); acc3 = fmaf(acc3, 0.9998f, 0.0625f);
     }
-    mean[v] = mv;
-    lsd[v] = lv;
-  }
-#endif
-#ifdef LNW_PROBE_DUMP
-  if (valid) {
-    float *dh = (float *)a.forced_act + rows * (64 + NI) + r * 8;
+  } else if (MODE == 2) {
+    for (int it = 0; it < 600; it++) {
+      const f32x4v v = *(const f32x4v *)(warea + ((lane + it) & 63) * KS + 4 * (it & 3));
+      acc0 += v[0]; acc1 += v[1]; acc2 += v[2]; acc3 += v[3];
+    }
+  } else if (MODE == 3) {
+    const float *q = pa.a.params + pa.off_w1;
+    for (int it = 0; it < 300; it++) {
+      const f32x4v v = *(const f32x4v *)(q + 4 * ((lane + 64 * it) & 4095));
+      acc0 += v[0]; acc1 += v[1]; acc2 += v[2]; acc3 += v[3];
+    }
+  } else if (MODE == 4) {
+    for (int it = 0; it < 100; it++) __builtin_amdgcn_s_sleep(8);
+  } else if (MODE == 6) {
+    for (int it = 0; it < 600; it++) {
+      acc0 = fmaf(acc0, 1.0001f, 0.5f);
+      warea[64 * KS + lane + 64 * (it % ((45 * 64 - 64 * KS) / 64 > 0 ? (45 * 64 - 64 * KS) / 64 : 1))] = acc0;
+    }
+  } else if (MODE == 7) {
+    float *o = pa.a.logp_out ? pa.a.logp_out + e * pa.a.act_env_stride + 4 * i : nullptr;
+    for (int it = 0; it < 300 && o; it++) {
+      acc0 = fmaf(acc0, 1.0001f, 0.5f);
+      o[it & 3] = acc0;
+    }
+  } else if (MODE == 8) {
+    for (int it = 0; it < 500; it++) {
+      acc0 = __builtin_amdgcn_exp2f(acc0 * 1e-3f); acc1 = __builtin_amdgcn_logf(acc1 + 1.f);
+      acc2 = __builtin_amdgcn_rcpf(acc2 + 1.f); acc3 = __builtin_amdgcn_sqrtf(acc3 + 1.f);
+    }
+  } else if (MODE == 9) {
+    unsigned h0 = (unsigned)lane, h1 = 7u;
+    for (int it = 0; it < 1000; it++) {
+      h0 = __umulhi(h0 ^ 0x9E3779B9u, 0xD2511F53u) + h1;
+      h1 = h1 * 0xCD9E8D57u + h0;
+    }
+    acc0 = (float)h0; acc1 = (float)h1;
+  } else {
+    bf16x8 w;
 #pragma unroll
-    for (int v = 0; v < NOUT; v++) { dh[v] = mean[v]; dh[4 + v] = lsd[v]; }
+    for (int j = 0; j < 8; j++) w[j] = (__bf16)(0.001f * (float)(lane + j));
+    f32x4v c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
+    for (int it = 0; it < 400; it++) {
+      c0 = mfma32(w, w, c0); c1 = mfma32(w, w, c1); c2 = mfma32(w, w, c2); c3 = mfma32(w, w, c3);
+    }
+    acc0 = c0[0] + c1[1] + c2[2] + c3[3];
   }
+  asm volatile("" ::"v"(acc0), "v"(acc1), "v"(acc2), "v"(acc3));
+}
+#endif
+
+// The phases of a block. PA_THREADS = 512 (one block per CU, two waves per
+// SIMD): every wave runs its head, then the waves of each SIMD run their MLPs
+// one at a time — a wave's MLP (v_mfma_f32_16x16x32_bf16 chains and the
+// ds_bpermute gather of the heads) while the other wave of its SIMD executed
+// anything at all came out nondeterministic in rows 48-63 (lanes 48-63: the
+// fourth 16-row tile) of one of the two waves (DESIGN.md "The policy reading
+// its rows in place"); with the partner parked at a barrier it is exact. The
+// SIMD of each wave comes from HW_ID, so nothing assumes how the hardware
+// deals waves to SIMDs; one MLP at a time per SIMD also holds for any dealing.
+template <int NI>
+__device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *P, float *warea, int lane, int g,
+                                             int m, bool valid, long long e, int i, long long istride, long long r0,
+                                             long long rows, float (&mean)[NOUT], float (&lsd)[NOUT]) {
+  constexpr int Q1 = NI / 16;
+  head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
+  if constexpr (PA_THREADS > 256) {
+    constexpr int NWB = PA_THREADS / WAVE;
+    __shared__ int simd_of[NWB];
+    const int wv = (int)(threadIdx.x / WAVE);
+    const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3);  // hwreg(HW_ID).SIMD_ID
+    if (lane == 0) simd_of[wv] = simd;
+    __syncthreads();
+    int rank = 0, nph = 1;  // this wave's turn on its SIMD; turns needed by the busiest SIMD
+#pragma unroll
+    for (int w2 = 0; w2 < NWB; w2++) {
+      int r2 = 0;
+#pragma unroll
+      for (int w3 = 0; w3 < w2; w3++) r2 += simd_of[w3] == simd_of[w2] ? 1 : 0;
+      nph = r2 + 1 > nph ? r2 + 1 : nph;
+      rank = w2 == wv ? r2 : rank;
+    }
+    for (int ph = 0; ph < nph; ph++) {
+      if (ph == rank) mlp_heads<Q1>(pa, warea, lane, g, m, mean, lsd);
+#ifdef LNW_PROBE_DISTURB  // diagnostics probes only (tools/build_probes.sh): the partner's work
+      else disturb<LNW_PROBE_DISTURB, NI + 4>(pa, warea, lane, e, i);
+#endif
+      __syncthreads();
+    }
+  } else {
+    mlp_heads<Q1>(pa, warea, lane, g, m, mean, lsd);
+  }
+}
+
+template <int NI>
+__global__ __launch_bounds__(PA_THREADS, 512 / PA_THREADS) void policy_act_kernel(PolicyArgs pa) {
+  constexpr int Q1 = NI / 16;        // fc1 k-quads (n_in zero-padded to NI)
+  constexpr int KS = NI + 4;         // row stride of the wave's fc1 input tile (16-B aligned)
+  const lnw_policy_args &a = pa.a;
+  const int n_in = pa.n_in;
+  const int n_par = CONV_PARAMS + 2 * n_in;
+  float *P = actor_lds;                // [n_par] conv head + LayerNorm parameters
+  // per wave: [45][64] pooled conv1 maps (one column per lane), then the
+  // wave's fc1 input tile [64][KS] over the same floats
+  constexpr int WAREA = (45 > KS ? 45 : KS) * WAVE;
+  float *warea = actor_lds + ((n_par + 3) & ~3) + (threadIdx.x / WAVE) * WAREA;
+  for (int i = threadIdx.x; i < n_par; i += blockDim.x) P[i] = a.params[i];
+  const int n = a.n, D = a.D;
+  const long long rows = a.E * n;
+  const long long r0 = (long long)blockIdx.x * PA_THREADS;
+  const long long istride = a.obs_in_env_stride ? a.obs_in_env_stride : (long long)n * D;
+  __syncthreads();
+  const int lane = threadIdx.x & (WAVE - 1), g = lane >> 4, m = lane & 15;
+  const long long r = r0 + threadIdx.x;
+  const bool valid = r < rows;  // (every lane stays for the wave-wide MFMAs)
+  // (32-bit: rows < 2^31, checked on the host; fewer registers live across the head)
+  const int e32 = valid ? (int)r / n : 0;
+  const long long e = e32;
+  const int i = valid ? (int)r - e32 * n : 0;
+  const long long E = a.E;
+  const bool alive = valid && a.alive[(long long)(a.own0 + i) * E + e] != 0;
+  const bool live = !a.live || (valid && a.live[e] != 0);
+  // ---- env-level side work by the lane of ship 0 ---------------------------
+  if (valid && i == 0) {
+    if (a.script) {  // scripted rows: profile j for red ship j < script_n, zeros past the table
+      for (int j = 0; j < a.script_cnt; j++) {
+        const int ag = a.script_own0 + j;
+        const bool al = a.alive[(long long)ag * E + e] != 0;
+        const bool has = j < a.script_n && a.t < a.script_steps;
+        f64x4 v = {0.0, 0.0, 0.0, 0.0};
+        if (al && has) v = *(const f64x4 *)(a.script + ((long long)j * a.script_steps + a.t) * 4);
+        *(f64x4 *)(a.full + (e * a.A + ag) * 4) = v;
+      }
+    }
+    if (a.kinds) {
+      bool all = true;
+      for (int ag = 0; ag < a.A; ag++) all = all && a.alive[(long long)ag * E + e] != 0;
+      const uint8_t k = (a.kinds_f32_all_alive && all) ? (uint8_t)LNW_KIND_F32 : (uint8_t)LNW_KIND_F64;
+      for (int ag = 0; ag < a.A; ag++) a.kinds[e * a.A + ag] = k;
+      if (a.f32_out) a.f32_out[e * a.f32_env_stride] = k == LNW_KIND_F32 ? 1 : 0;
+    }
+  }
+  // ---- head, fc1 tile and MLP (phases: head_and_mlp) --------------------------
+  float mean[NOUT], lsd[NOUT];
+#ifdef LNW_PROBE_NOMLP  // timing / diagnostics probes only: no MLP (the lane's own fc1 tile row)
+  head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
+  for (int v = 0; v < NOUT; v++) {
+    mean[v] = warea[lane * KS + 12 + v];
+    lsd[v] = 0.f;
+  }
+#else
+  head_and_mlp<NI>(pa, P, warea, lane, g, m, valid, e, i, istride, r0, rows, mean, lsd);
 #endif
   if (!valid) return;
+  // the row's env and ship again, from an opaque copy of the row index: so
+  // they are recomputed here instead of living across the head (where the
+  // register file is full and they would go to scratch)
+  int r_o = (int)(blockIdx.x * PA_THREADS + threadIdx.x);
+  asm volatile("" : "+v"(r_o));
+  const int e_o = r_o / n, i_o = r_o - e_o * n;
   float std_[NOUT];
   bool ok = true;
 #pragma unroll
@@ -560,7 +715,7 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   // ---- sample / forced actions and log-probabilities -----------------------
   float act[NOUT], lp[NOUT];
   if (a.forced) {  // MLP.get_dist (network.py:117-152): no NaN guard
-    const float *fa = a.forced_act + e * a.fa_env_stride + 4 * i;
+    const float *fa = a.forced_act + (long long)e_o * a.fa_env_stride + 4 * i_o;
 #pragma unroll
     for (int o = 0; o < NOUT; o++) act[o] = fa[o];
   } else {
@@ -570,7 +725,7 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
     }
     const unsigned long long call = a.call_dev ? (unsigned long long)*a.call_dev : 0ull;
     const unsigned long long slot = (call * (unsigned long long)a.T + (unsigned long long)a.t) * 4ull;
-    const long long grow = a.row_base + r;
+    const long long grow = a.row_base + r_o;
     float eps[NOUT];
     keyed_eps(a.seed, slot + (unsigned long long)a.which, grow, eps);
 #pragma unroll
@@ -596,13 +751,13 @@ __global__ __launch_bounds__(CH_THREADS, 2) void policy_act_kernel(PolicyArgs pa
   if (a.full) {
     f64x4 v = {alive ? (double)act[0] : 0.0, alive ? (double)act[1] : 0.0, alive ? (double)act[2] : 0.0,
                alive ? (double)act[3] : 0.0};
-    *(f64x4 *)(a.full + (e * a.A + a.own0 + i) * 4) = v;
+    *(f64x4 *)(a.full + ((long long)e_o * a.A + a.own0 + i_o) * 4) = v;
   }
   if (a.act_out)
-    *(f32x4 *)(a.act_out + e * a.act_env_stride + 4 * i) =
+    *(f32x4 *)(a.act_out + (long long)e_o * a.act_env_stride + 4 * i_o) =
         keep ? f32x4{act[0], act[1], act[2], act[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
   if (a.logp_out)
-    *(f32x4 *)(a.logp_out + e * a.act_env_stride + 4 * i) =
+    *(f32x4 *)(a.logp_out + (long long)e_o * a.act_env_stride + 4 * i_o) =
         keep ? f32x4{lp[0], lp[1], lp[2], lp[3]} : f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
@@ -666,7 +821,7 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_arg
           acc[rt][1] = mfma4(w1[v], xb[rt][v], acc[rt][1]);
         }
     }
-#pragma unroll
+  #pragma unroll
     for (int rt = 0; rt < 4; rt++)
 #pragma unroll
       for (int nt = 0; nt < 2; nt++) part[((w * 2 + nt) * 4 + rt) * WAVE + lane] = acc[rt][nt];
@@ -686,7 +841,7 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_arg
 #pragma unroll
       for (int rt = 0; rt < 4; rt++) t2[rt][0] = bv;
       mfma_layer<1, 2>((const f32x4v *)(C + co.w2) + nt * 2 * WAVE, h1, t2, lane);
-#pragma unroll
+    #pragma unroll
       for (int rt = 0; rt < 4; rt++) {
 #pragma unroll
         for (int v = 0; v < 4; v++) t2[rt][0][v] = tanh_fast(t2[rt][0][v]);
@@ -707,7 +862,7 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_arg
 #pragma unroll
       for (int rt = 0; rt < 4; rt++) t3[rt][0] = bv;
       mfma_layer<1, 4>((const f32x4v *)(C + co.w3) + nt * 4 * WAVE, h2, t3, lane);
-      const f32x4v w4 = *(const f32x4v *)(C + co.w4 + nt * 16 + 4 * g);
+          const f32x4v w4 = *(const f32x4v *)(C + co.w4 + nt * 16 + 4 * g);
 #pragma unroll
       for (int rt = 0; rt < 4; rt++)
 #pragma unroll
@@ -754,11 +909,16 @@ int lnw_actor_features(const float *params_dev, int32_t obs_dim, const float *ob
   if (!params_dev || !obs_dev || !out_dev || B < 0) return LNW_EINVAL;
   if (obs_dim < WIN || obs_dim - WIN + 12 > MAX_IN) return LNW_EUNSUPPORTED;
   if (B == 0) return 0;
-  long long blocks = (B + CH_THREADS - 1) / CH_THREADS;
-  if (blocks > 8192) blocks = 8192;
+  const long long blocks = (B + CH_THREADS - 1) / CH_THREADS;  // one row per thread
+  if (B >= (1ll << 31) - CH_THREADS) return LNW_EUNSUPPORTED;  // (32-bit rows)
   const int n_par = CONV_PARAMS + 2 * (obs_dim - WIN + 12);
-  features_kernel<<<dim3((unsigned)blocks), dim3(CH_THREADS), (n_par + 45 * CH_THREADS) * sizeof(float),
-                    (hipStream_t)stream>>>(params_dev, obs_dim, obs_dev, B, bn_running, out_dev);
+  const size_t lds = (n_par + 45 * CH_THREADS) * sizeof(float);
+  if (obs_dim - WIN + 12 <= 32)
+    features_kernel<32><<<dim3((unsigned)blocks), dim3(CH_THREADS), lds, (hipStream_t)stream>>>(
+        params_dev, obs_dim, obs_dev, (int)B, bn_running, out_dev);
+  else
+    features_kernel<MAX_IN><<<dim3((unsigned)blocks), dim3(CH_THREADS), lds, (hipStream_t)stream>>>(
+        params_dev, obs_dim, obs_dev, (int)B, bn_running, out_dev);
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 
@@ -796,13 +956,17 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   pa.off_b1 = o; o += FC1 + FC2 + FC3;
   pa.off_w1 = o;
   const long long rows = a.E * a.n;
-  const unsigned blocks = (unsigned)((rows + CH_THREADS - 1) / CH_THREADS);
+  if (rows + PA_THREADS >= (1ll << 31)) return LNW_EUNSUPPORTED;  // (32-bit row indices)
+  const unsigned blocks = (unsigned)((rows + PA_THREADS - 1) / PA_THREADS);
   const int npar4 = (CONV_PARAMS + 2 * pa.n_in + 3) & ~3;
-  const size_t lds = (size_t)(npar4 + (CH_THREADS / WAVE) * (pa.n_in <= 32 ? 45 : MAX_IN + 4) * WAVE) * sizeof(float);
+  size_t lds = (size_t)(npar4 + (PA_THREADS / WAVE) * (pa.n_in <= 32 ? 45 : MAX_IN + 4) * WAVE) * sizeof(float);
+#ifdef LNW_PROBE_ONEBLOCK  // probe builds: one block per CU
+  if (lds < 84 * 1024) lds = 84 * 1024;
+#endif
   if (pa.n_in <= 32)
-    policy_act_kernel<32><<<blocks, CH_THREADS, lds, (hipStream_t)stream>>>(pa);
+    policy_act_kernel<32><<<blocks, PA_THREADS, lds, (hipStream_t)stream>>>(pa);
   else
-    policy_act_kernel<MAX_IN><<<blocks, CH_THREADS, lds, (hipStream_t)stream>>>(pa);
+    policy_act_kernel<MAX_IN><<<blocks, PA_THREADS, lds, (hipStream_t)stream>>>(pa);
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 

@@ -2936,9 +2936,13 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // observation passes go through one workgroup-wide queue that every free wave
 // of a quiet unit serves, so the CU's units finish their stream together
 // instead of 4-5 us apart (the spread of separate workgroups on one CU).
-template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false>
-__global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 0 ? 2 : 1) void step_kernel(
-    KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
+// SEQ: the body of one step inside lnw_step_seq's loop (step_kernel SEQ, below):
+// a wave that leaves the step early then still meets every barrier its
+// partner wave reaches later in the same step (phase O's), since both go on to
+// the next step instead of exiting.
+template <int NB, int NR, bool CW, bool REFW, int UN, bool PS, bool SEQ>
+__device__ __forceinline__ void step_body(
+    const KParams &P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
   static_assert(UN == 1 || (NB > 0 && EPW == WAVE && !REFW), "units need the two-wave templated kernel");
   const int unit = UN > 1 ? (int)(threadIdx.x / (2 * WAVE)) : 0;
@@ -3073,11 +3077,14 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
   // After a second barrier wave 0 merges red's hits, sums, counter and cells and
   // runs the tail. (The analytics logs' records then interleave the two sides'
   // turns; their order across envs is the atomics' order anyway.)
+  // (rows written after phase S by wave 0 alone, behind a barrier: phase O)
+  const bool phase_o = !((P.dbg_skip & 1) || emit || P.no_obs);
   if (wid == 1 && !psplit) {
     if constexpr (ST) {
       if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
     }
     prof_stamp(S, 5);
+    if (SEQ && phase_o) __syncthreads();  // wave 0's phase-O barrier
     return;
   }
   if (!qcap && astar && !(P.dbg_skip & 4)) {
@@ -3298,7 +3305,10 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
           for (int a = 0; a < NB; a++) turn(X, a, N, ev, hits, bsx, bsy, nbp, rsx, rsy, nrp, tp, t0);
         }
         __syncthreads();
-        if (wid == 1) return;
+        if (wid == 1) {
+          if (SEQ && phase_o) __syncthreads();  // wave 0's phase-O barrier
+          return;
+        }
         {
           const uint32_t w0 = COLW(cr.pos_cur, 0), w1 = COLW(cr.pos_cur, 1), w2 = COLW(cr.pos_cur, 2),
                          w3 = COLW(cr.pos_cur, 3);
@@ -3440,11 +3450,43 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
       for (int q = 0; q < 4; q++) prof_put(S, 16 + q, tp[q]);
   }
   prof_stamp(S, 3);
-  if ((P.dbg_skip & 1) || emit || P.no_obs) return;
+  if (!phase_o) return;
   __syncthreads();
   // ---- phase O: observations ---------------------------------------------
   if constexpr (ST) write_obs_t<NB, NR>(P, S, c, duct_col, obs_b, obs_r, env0, nenv);
   else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
+}
+
+// One step (SEQ = false: lnw_step), or P.seq_steps steps in one launch
+// (lnw_step_seq): each workgroup steps its own envs through the sequence, step
+// k reading action array k and writing output set k (the P.seq_* strides), so
+// the results are those of seq_steps lnw_step calls. Between steps the
+// workgroup's state stores are drained (vmcnt(0)) before a barrier, and the next
+// step's phase L reads them back through the same CU. No grid-wide barrier: the
+// workgroups drift apart, so one CU's head overlaps another's observation stream
+// and the launch gaps of separate step launches disappear.
+template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false, bool SEQ = false>
+__global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 0 ? 2 : 1) void step_kernel(
+    KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
+    float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
+  if constexpr (!SEQ) {
+    step_body<NB, NR, CW, REFW, UN, PS, false>(P, S, actions, row_kind, obs_b, obs_r, rew_b, rew_r, done_out,
+                                               cog_out);
+  } else {
+    const long long asz = P.act_dtype == LNW_ACT_F64 ? 8 : 4, rsz = P.rew_f64 ? 8 : 4;
+    for (int k = 0; k < P.seq_steps; k++) {
+      auto adv = [&](void *p, long long stride, long long sz) {
+        return p ? (void *)((char *)p + (long long)k * stride * sz) : nullptr;
+      };
+      step_body<NB, NR, CW, REFW, UN, PS, true>(
+          P, S, adv(actions, P.seq_act, asz), (const uint8_t *)adv((void *)row_kind, P.seq_kind, 1),
+          (float *)adv(obs_b, P.seq_obs[0], 4), (float *)adv(obs_r, P.seq_obs[1], 4),
+          (float *)adv(rew_b, P.seq_rew[0], rsz), (float *)adv(rew_r, P.seq_rew[1], rsz),
+          (int32_t *)adv(done_out, P.seq_done, 4), (float *)adv(cog_out, P.seq_cog, rsz));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's state stores done
+      __syncthreads();
+    }
+  }
 }
 
 #include "lnw_group.inc"
@@ -4507,9 +4549,14 @@ int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn
   return 0;
 }
 
-int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
-             float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
-             int32_t *done_dev, float *cog_dev, void *stream) {
+namespace {
+constexpr int STEP_NOT_FUSED = 1;  // step_launch: this shape has no fused sequence kernel
+// lnw_step's launch; with seq (lnw_step_seq) the fused sequence kernel when the
+// shape has one (units kernel, templated 4v4 default variant), else
+// STEP_NOT_FUSED before anything is launched
+int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t action_dtype,
+                const uint8_t *row_kind_dev, float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev,
+                float *rew_red_dev, int32_t *done_dev, float *cog_dev, void *stream) {
   if (!h || !actions_dev) return fail(LNW_EINVAL, "null argument");
   if (!h->terrain) return fail(LNW_ESTATE, "lnw_load_terrain must be called first");
   if (action_dtype != LNW_ACT_F32 && action_dtype != LNW_ACT_F64 && action_dtype != LNW_ACT_I32)
@@ -4525,6 +4572,18 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   k.no_obs = obs_blue_dev == nullptr ? 1 : 0;
   k.dbg_skip = h->dbg_skip;
   k.store_wt = h->store_wt;
+  k.seq_steps = 1;
+  if (seq) {
+    k.seq_steps = seq->steps;
+    k.seq_act = seq->act_step;
+    k.seq_kind = seq->kind_step;
+    k.seq_obs[0] = seq->obs_blue_step;
+    k.seq_obs[1] = seq->obs_red_step;
+    k.seq_rew[0] = seq->rew_blue_step;
+    k.seq_rew[1] = seq->rew_red_step;
+    k.seq_done = seq->done_step;
+    k.seq_cog = seq->cog_step;
+  }
   KState s = make_state(h);
   size_t lds = step_launch_lds_bytes(h, k.epw);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
@@ -4538,6 +4597,9 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
   // the units kernel (LNW_NO_UNITS keeps one unit per workgroup)
   const bool units = templated && h->nb == 4 && !h->contact && !h->no_units && h->units_fit && k.epw == EPW &&
                      k.los_mode == 0 && h->E % (EPW * UNITS) == 0 && !(h->dbg_skip & (1 | 2 | 512));
+  // lnw_step_seq's fused kernels: the units kernel and the templated 4v4 default variant
+  const bool seq_fused = units || (templated && h->nb == 4 && !h->contact && k.los_mode != 2);
+  if (seq && (!seq_fused || h->prof)) return STEP_NOT_FUSED;
   // per-unit records (LNW_PROF) of the kernel launched below (the group kernel has its own grid)
   const unsigned nwg = use_group ? (unsigned)((h->E + GEPW - 1) / GEPW) : grid.x;
   if (h->prof) {
@@ -4560,7 +4622,16 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
                    : k.los_mode == 2 ? LNW_KERNEL_REFLOS
                    : templated ? (cw ? LNW_KERNEL_TEAM_CONTACT : LNW_KERNEL_TEAM)
                    : use_group ? LNW_KERNEL_GROUP : LNW_KERNEL_GENERIC;
-  if (units) {
+  if (units && seq) {
+    step_kernel<4, 4, false, false, UNITS, false, true><<<dim3(h->E / (EPW * UNITS)), dim3(2 * WAVE * UNITS),
+                                                          (size_t)UNITS * ((lds + 15) & ~(size_t)15), st>>>(
+        k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev,
+        cog_dev);
+  } else if (seq) {
+    step_kernel<4, 4, false, false, 1, false, true><<<grid, dim3(2 * WAVE), lds, st>>>(
+        k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev,
+        cog_dev);
+  } else if (units) {
     // 4 units of 64 envs per workgroup, one workgroup per CU (step_kernel UN)
     step_kernel<4, 4, false, false, UNITS><<<dim3(h->E / (EPW * UNITS)), dim3(2 * WAVE * UNITS),
                                              (size_t)UNITS * ((lds + 15) & ~(size_t)15), st>>>(
@@ -4595,6 +4666,44 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
 #undef LNW_STEP
   HIPCHK(hipGetLastError());
   if (s.prof) prof_report(h, st, (int)nwg);
+  return 0;
+}
+}  // namespace
+
+int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
+             float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
+             int32_t *done_dev, float *cog_dev, void *stream) {
+  return step_launch(h, nullptr, actions_dev, action_dtype, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev,
+                     rew_red_dev, done_dev, cog_dev, stream);
+}
+
+int lnw_step_seq(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t action_dtype,
+                 const uint8_t *row_kind_dev, float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev,
+                 float *rew_red_dev, int32_t *done_dev, float *cog_dev, void *stream) {
+  if (!h || !seq) return fail(LNW_EINVAL, "null argument");
+  if (seq->steps < 1) return fail(LNW_EINVAL, "seq->steps must be >= 1");
+  if (seq->act_step < 0 || seq->kind_step < 0 || seq->obs_blue_step < 0 || seq->obs_red_step < 0 ||
+      seq->rew_blue_step < 0 || seq->rew_red_step < 0 || seq->done_step < 0 || seq->cog_step < 0)
+    return fail(LNW_EINVAL, "negative step stride");
+  const int rc = step_launch(h, seq, actions_dev, action_dtype, row_kind_dev, obs_blue_dev, obs_red_dev,
+                             rew_blue_dev, rew_red_dev, done_dev, cog_dev, stream);
+  if (rc != STEP_NOT_FUSED) return rc;
+  // no fused kernel for this shape: K launches
+  const long long asz = action_dtype == LNW_ACT_F64 ? 8 : 4, rsz = h->kp.rew_f64 ? 8 : 4;
+  for (int k = 0; k < seq->steps; k++) {
+    auto adv = [&](const void *p, long long stride, long long sz) {
+      return p ? (void *)((char *)p + (long long)k * stride * sz) : nullptr;
+    };
+    if (int e = step_launch(h, nullptr, adv(actions_dev, seq->act_step, asz), action_dtype,
+                            (const uint8_t *)adv(row_kind_dev, seq->kind_step, 1),
+                            (float *)adv(obs_blue_dev, seq->obs_blue_step, 4),
+                            (float *)adv(obs_red_dev, seq->obs_red_step, 4),
+                            (float *)adv(rew_blue_dev, seq->rew_blue_step, rsz),
+                            (float *)adv(rew_red_dev, seq->rew_red_step, rsz),
+                            (int32_t *)adv(done_dev, seq->done_step, 4), (float *)adv(cog_dev, seq->cog_step, rsz),
+                            stream))
+      return e;
+  }
   return 0;
 }
 

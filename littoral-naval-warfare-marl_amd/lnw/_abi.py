@@ -24,7 +24,7 @@ LNW_NFIELDS = 14
 # exported symbols (must match include/lnw.h)
 SYMBOLS = [
     "lnw_abi_version", "lnw_last_error", "lnw_create", "lnw_destroy", "lnw_load_terrain",
-    "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_observe", "lnw_observe_ex", "lnw_state_field", "lnw_tlist_cap",
+    "lnw_set_rng", "lnw_reset", "lnw_step", "lnw_step_seq", "lnw_observe", "lnw_observe_ex", "lnw_state_field", "lnw_tlist_cap",
     "lnw_set_epw", "lnw_set_variant", "lnw_set_reward_dtype",
     "lnw_set_counters",
     "lnw_los_batch", "lnw_astar_batch", "lnw_move_batch", "lnw_path_query", "lnw_los_query", "lnw_copy",
@@ -56,6 +56,12 @@ class Spawn(C.Structure):
     _fields_ = [("types", C.c_int32 * 64), ("pos", (C.c_int32 * 2) * 64),
                 ("rand_ls", C.c_int32 * 64), ("box_lo", C.c_int32 * 2),
                 ("box_hi", C.c_int32 * 2)]
+
+
+class Seq(C.Structure):  # include/lnw.h: lnw_seq
+    _fields_ = [("steps", C.c_int32), ("act_step", C.c_int64), ("kind_step", C.c_int64),
+                ("obs_blue_step", C.c_int64), ("obs_red_step", C.c_int64), ("rew_blue_step", C.c_int64),
+                ("rew_red_step", C.c_int64), ("done_step", C.c_int64), ("cog_step", C.c_int64)]
 
 
 class PolicyArgs(C.Structure):  # include/lnw.h: lnw_policy_args
@@ -111,6 +117,7 @@ def load(path=None):
         "lnw_set_rng": ([P, I32, U64, P, P], C.c_int),
         "lnw_reset": ([P, P, C.POINTER(Spawn), P, P], C.c_int),
         "lnw_step": ([P, P, I32, P, P, P, P, P, P, P, P], C.c_int),
+        "lnw_step_seq": ([P, C.POINTER(Seq), P, I32, P, P, P, P, P, P, P, P], C.c_int),
         "lnw_observe": ([P, I32, P, P, P], C.c_int),
         "lnw_observe_ex": ([P, I32, P, C.c_int64, P, C.c_int64, P], C.c_int),
         "lnw_state_field": ([P, I32, C.POINTER(P), C.POINTER(I64)], C.c_int),

@@ -204,6 +204,44 @@ class BatchedGame:
                               torch.cuda.current_stream(self.device).cuda_stream))
         return self._outd
 
+    def step_seq(self, actions, row_kind=None, obs=True, keep="last"):
+        """K Game.step calls on an action sequence known ahead of time
+        (lnw_step_seq): actions [K, E, A, 4] (contiguous cuda, the step()
+        dtypes), row_kind [K, E, A] or None. The results are those of K step()
+        calls; the rows of a step are mutated where step() mutates them.
+        keep="last": every step writes the game's output tensors (so they end
+        holding step K-1's outputs, as after K step() calls); keep="all":
+        returns new tensors with every step's outputs, [K, ...]."""
+        a = actions
+        if a.dim() != 4 or a.shape[1:] != self._ashape or not a.is_cuda or not a.is_contiguous():
+            raise ValueError(f"actions must be a contiguous cuda tensor of shape (K, {tuple(self._ashape)})")
+        dt = self._dtypes.get(a.dtype)
+        if dt is None:
+            raise TypeError(f"unsupported action dtype {a.dtype}")
+        K = a.shape[0]
+        rk = None
+        sq = _abi.Seq(K, self.E * self.A * 4, 0, 0, 0, 0, 0, 0, 0)
+        if row_kind is not None:
+            rkt = torch.as_tensor(row_kind, dtype=torch.uint8, device=self.device).contiguous()
+            assert rkt.shape == (K, self.E, self.A)
+            rk, sq.kind_step = _ptr(rkt), self.E * self.A
+        if keep == "last":
+            out = self._outd
+        elif keep == "all":
+            out = {k: torch.zeros((K,) + tuple(v.shape), dtype=v.dtype, device=self.device)
+                   for k, v in self._outd.items()}
+            sq.obs_blue_step, sq.obs_red_step = self.E * self.nb * self.Db, self.E * self.nr * self.Dr
+            sq.rew_blue_step, sq.rew_red_step = self.E * self.nb, self.E * self.nr
+            sq.done_step = sq.cog_step = self.E
+        else:
+            raise ValueError("keep must be 'last' or 'all'")
+        p = {k: _ptr(v) for k, v in out.items()}
+        ob, orr = (p["obs_blue"], p["obs_red"]) if obs else (None, None)
+        check(self.L.lnw_step_seq(self.h, C.byref(sq), a.data_ptr(), dt, rk, ob, orr, p["rew_blue"],
+                                  p["rew_red"], p["done"], p["cog"],
+                                  torch.cuda.current_stream(self.device).cuda_stream))
+        return out
+
     # ---------------------------------------------------------- analytics
     def enable_analytics(self, eng_cap=1 << 20, ew_cap=1 << 20, maps=True):
         """Bind device buffers for the reference's analytics side channels
@@ -367,10 +405,13 @@ class BatchedGame:
         # the observation buffers are sized by this game's ship types: a
         # snapshot of another fleet (a medium side has shorter rows) is refused
         # here, before the library would select kernels for its row length
+        # (header: magic, version, then E, nb, nr as int32 at bytes 12..23; a
+        # snapshot of another shape is left to the library to refuse)
+        hdr = buf[:24].cpu().view(torch.int32).tolist() if buf.numel() >= 24 else []
         off = 256
         for f in range(_abi.LNW_NFIELDS):
             off += (self._field(f)[1] + 255) & ~255
-        if buf.numel() >= off + 4 * self.A:
+        if hdr[3:6] == [self.E, self.nb, self.nr] and buf.numel() >= off + 4 * self.A:
             types = buf[off:off + 4 * self.A].cpu().view(torch.int32).tolist()
             if types != [int(t) for t in self.blue_types + self.red_types]:
                 raise ValueError(f"snapshot fleet {types} differs from this game's "

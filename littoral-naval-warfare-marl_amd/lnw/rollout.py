@@ -310,7 +310,7 @@ def gae(rewards, values, gamma, lambda_=0.95):
 # The rollout's fast path observes into the buffer directly and the policy
 # reads the rows there (obs_in_env_stride); off: the rows go to the game's
 # packed observation buffer and the policy copies them.
-STRIDED_POLICY_INPUT = False
+STRIDED_POLICY_INPUT = True
 
 
 class Rollout:

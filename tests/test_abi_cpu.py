@@ -32,7 +32,7 @@ def test_header_symbols_match_binding():
 def test_library_exports_every_header_symbol(L):
     for s in header_symbols():
         assert hasattr(L, s), s
-    assert L.lnw_abi_version() == 4
+    assert L.lnw_abi_version() == 5
 
 
 def test_hit_tables_match_numpy(L):

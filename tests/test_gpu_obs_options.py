@@ -135,44 +135,66 @@ def test_observe_ex_strided_rows_and_null_side(name):
     g2.close()
 
 
-def test_policy_act_strided_input_equals_packed():
+@pytest.mark.parametrize("with_live", [True, False])
+def test_policy_act_strided_input_equals_packed(with_live):
     """lnw_policy_act reading its rows from a [E][T][n][D] rollout buffer at
-    step t (obs_in_env_stride) gives the outputs of the packed [E][n][D] rows,
-    and in place (obs_out == obs) leaves live envs' rows alone and zeroes the
-    ended ones."""
+    step t (obs_in_env_stride) gives the outputs of the packed [E][n][D] rows
+    bit for bit, call after call, and in place (obs_out == obs) leaves live
+    envs' rows alone and zeroes the ended ones. E = 32 768 (config 5's size):
+    two blocks per CU, the shape at which the round-4 kernel's spilled
+    registers came back wrong in lanes 48-63 of the second block's waves
+    (DESIGN.md, "The policy reading its rows in place")."""
     import ctypes as C
     from lnw import _abi
     from lnw.rollout import BatchedActor
     L = _abi.load()
     torch.manual_seed(7)
     a = BatchedActor.for_obs(68).cuda()
-    E, n, D, T, t = 700, 4, 68, 6, 2
+    E, n, D, T, t = 32768, 4, 68, 40, 5
     obs = torch.rand((E, n, D), device="cuda")
     obs[:, :, :49] = torch.randint(0, 256, (E, n, 49), device="cuda") / 255.0
     buf = torch.rand((E, T, n, D), device="cuda")
     buf[:, t] = obs
     act = torch.rand((E, n, 4), device="cuda")
-    alive = torch.ones((n, E), dtype=torch.uint8, device="cuda")
+    alive = torch.ones((2 * n, E), dtype=torch.uint8, device="cuda")
     live = torch.ones(E, dtype=torch.uint8, device="cuda")
     live[::5] = 0
     params = a.packed_policy()
+    call = torch.zeros(1, dtype=torch.int64, device="cuda")
     res = []
-    for strided in (False, True):
+    for rep, strided in enumerate([False] + [True] * 6):
         lp = torch.zeros((E, n, 4), device="cuda")
+        ac = torch.zeros((E, n, 4), device="cuda")
+        full = torch.zeros((E, 2 * n, 4), dtype=torch.float64, device="cuda")
         pa = _abi.PolicyArgs()
         src = buf.data_ptr() + t * n * D * 4 if strided else obs.data_ptr()
-        pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = src, E, n, D, 0, n
+        pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = src, E, n, D, 0, 2 * n
         pa.obs_in_env_stride = T * n * D if strided else 0
-        pa.params, pa.forced, pa.forced_act, pa.fa_env_stride = params.data_ptr(), 1, act.data_ptr(), n * 4
-        pa.alive, pa.logp_out, pa.act_env_stride = alive.data_ptr(), lp.data_ptr(), n * 4
-        pa.live = live.data_ptr()
+        # sampled (keyed) actions, as the rollout draws them; the log-probabilities
+        # and the f64 action array come out of the whole kernel
+        pa.params, pa.noise, pa.seed, pa.call_dev, pa.T, pa.t = params.data_ptr(), 0.05, 99, call.data_ptr(), T, t
+        pa.alive, pa.act_out, pa.logp_out, pa.act_env_stride = alive.data_ptr(), ac.data_ptr(), lp.data_ptr(), n * 4
+        pa.full = full.data_ptr()
+        if with_live:
+            pa.live = live.data_ptr()
         if strided:
             pa.obs_out, pa.obs_env_stride = src, T * n * D
         _abi.check(L.lnw_policy_act(C.byref(pa), None))
         torch.cuda.synchronize()
-        res.append(lp)
-    assert torch.equal(res[0], res[1])
-    keep = live.bool()
-    assert torch.equal(buf[keep, t], obs[keep]) and not buf[~keep, t].any()
+        res.append((ac, lp, full))
+    # (with live flags the first in-place call zeroes the ended envs' rows, so
+    # later calls read zeros there: their f64 action rows are compared on live
+    # envs; act / log-prob rows of ended envs are zero either way)
+    rowmask = (live.bool() if with_live else torch.ones(E, dtype=torch.bool, device="cuda"))
+    for k in range(1, len(res)):
+        for x, y in zip(res[0], res[k]):
+            m = rowmask[:, None].expand(E, x.shape[1]).reshape(-1)
+            bad = ((x != y).reshape(E * x.shape[1], -1).any(1) & m).nonzero().flatten()
+            assert bad.numel() == 0, f"call {k}: rows {bad[:6].tolist()} differ"
+    if with_live:
+        keep = live.bool()
+        assert torch.equal(buf[keep, t], obs[keep]) and not buf[~keep, t].any()
+    else:
+        assert torch.equal(buf[:, t], obs)
     others = [s for s in range(T) if s != t]
     assert not (buf[:, others] == 0).all()

@@ -38,13 +38,18 @@ def test_rollout_matches_reference(name, impl):
     _rollout_case(name, impl)
 
 
+@pytest.mark.parametrize("strided", [True, False])
 @pytest.mark.parametrize("name", ["4v4_trained_contact", "4v4_melee_done"])
-def test_rollout_contact_variant_matches_reference(name):
+def test_rollout_contact_variant_matches_reference(name, strided, monkeypatch):
     """The contact variant's kernels on the same recorded rollouts, without a
     per-step callback: the rollout's fast path (steps without rows, whose phase S
-    splits by side, and the two-wave observe), tape mode. The draw counters are
-    checked through every value the draws feed (a finished env's later draws
-    belong to no reference episode, so the final counter is not compared)."""
+    splits by side, and the two-wave observe), tape mode, with the policy reading
+    its rows where lnw_observe_ex left them in the rollout buffer (strided) or
+    from the game's packed buffer. The draw counters are checked through every
+    value the draws feed (a finished env's later draws belong to no reference
+    episode, so the final counter is not compared)."""
+    from lnw import rollout
+    monkeypatch.setattr(rollout, "STRIDED_POLICY_INPUT", strided)
     _rollout_case(name, "hip", contact=True)
 
 

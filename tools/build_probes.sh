@@ -1,6 +1,6 @@
 # Probe builds of lnw_actor.hip alone (tools/policy_probe.py timing,
 # tools/policy_determinism.py diagnostics): base, no conv head
-# (LNW_PROBE_NOCONV), no MLP (LNW_PROBE_NOMLP), per-stage dumps (LNW_PROBE_DUMP)
+# (LNW_PROBE_NOCONV), no MLP (LNW_PROBE_NOMLP)
 set -e
 cd "$(dirname "$0")/.."
 C=littoral-naval-warfare-marl_amd/csrc
@@ -9,5 +9,10 @@ mkdir -p tools/probe
 /opt/rocm/bin/hipcc $F $C/lnw_actor.hip -o tools/probe/actor_base.so &
 /opt/rocm/bin/hipcc $F -DLNW_PROBE_NOCONV $C/lnw_actor.hip -o tools/probe/actor_NOCONV.so &
 /opt/rocm/bin/hipcc $F -DLNW_PROBE_NOMLP $C/lnw_actor.hip -o tools/probe/actor_NOMLP.so &
-/opt/rocm/bin/hipcc $F -DLNW_PROBE_DUMP $C/lnw_actor.hip -o tools/probe/actor_dump.so &
+
+wait
+# the partner wave's work while a wave runs its MLP (LNW_PROBE_DISTURB modes)
+for d in 1 2 3 4 5 6 7 8 9; do
+  /opt/rocm/bin/hipcc $F -DLNW_PROBE_DISTURB=$d $C/lnw_actor.hip -o tools/probe/actor_disturb$d.so &
+done
 wait

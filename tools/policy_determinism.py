@@ -3,9 +3,8 @@
 strided in place like the rollout's direct path) -- are the outputs
 bit-identical from call to call?
 usage: python tools/policy_determinism.py [E] [reps] [variants,...]
-POLICY_LIB=path: an lnw_actor.hip-only build (tools/probe); with a build made
-with -DLNW_PROBE_DUMP, PROBE_DUMP=1 also compares the window each row read,
-its LayerNorm output and its heads, and checks the window against the input."""
+POLICY_LIB=path: an lnw_actor.hip-only build (tools/probe). Differing rows are
+reported with their 64-row waves."""
 import ctypes as C
 import os
 import sys
@@ -25,7 +24,6 @@ def main():
         print("lib", path, flush=True)
     else:
         L = _abi.load()
-    dump = os.environ.get("PROBE_DUMP") == "1"
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     n, D, T, t = 4, 68, 40, 5
@@ -40,15 +38,40 @@ def main():
     live = torch.ones(E, dtype=torch.bool, device="cuda")
     call = torch.zeros(1, dtype=torch.int64, device="cuda")
     out2 = torch.zeros((E, T, n, D), device="cuda")
-    dbg = torch.zeros(rows * (64 + 32 + 8), device="cuda") if dump else None
     variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["packed", "strided", "strided_sync",
                                                                    "strided_copy", "packed_inplace",
                                                                    "strided_nolive", "strided_noout"]
+    if "critic" in variants:  # lnw_rollout_post's critic (MFMA f32), strided rollout-buffer rows
+        from lnw.rollout import BatchedCritic
+        variants = [v for v in variants if v != "critic"]
+        cp = BatchedCritic(n * D).cuda().packed(n, D)
+        val = torch.zeros((E, T), device="cuda")
+        ref = None
+        nd = 0
+        for k in range(reps):
+            buf[:, t] = obs
+            val.zero_()
+            pp = _abi.RolloutPostArgs()
+            pp.obs, pp.obs_env_stride, pp.E, pp.n, pp.D = buf.data_ptr() + t * n * D * 4, T * n * D, E, n, D
+            pp.critic, pp.val, pp.val_env_stride = cp.data_ptr(), val.data_ptr() + t * 4, T
+            assert L.lnw_rollout_post(C.byref(pp), None) == 0
+            torch.cuda.synchronize()
+            cur = val[:, t].clone()
+            if ref is None:
+                ref = cur
+                continue
+            if not torch.equal(cur, ref):
+                d = (cur != ref).nonzero()[:, 0]
+                nd += 1
+                if nd <= 6:
+                    print("critic rep", k, len(d), "envs differ, max |d|", float((cur - ref).abs().max()),
+                          "envs", d[:6].tolist(), "lanes", sorted(set((d % 64).tolist()))[:8], flush=True)
+        print("critic mismatching reps:", nd, "of", reps - 1, flush=True)
     for var in variants:
         strided = var.startswith("strided")
         ref = None
         nd = 0
-        waves = set()
+        waves, lanes = set(), set()
         for k in range(reps):
             buf[:, t] = obs
             if var == "strided_sync":
@@ -71,25 +94,12 @@ def main():
                 pa.live = None
             if var == "strided_noout":
                 pa.obs_out = None
-            if dump:
-                dbg.zero_()
-                pa.forced_act = dbg.data_ptr()
             pa.act_out, pa.logp_out, pa.act_env_stride = acts.data_ptr() + t * n * 16, logp.data_ptr() + t * n * 16, T * n * 4
             pa.full = full.data_ptr()
             assert L.lnw_policy_act(C.byref(pa), None) == 0
             torch.cuda.synchronize()
             cur = [acts[:, t].clone(), logp[:, t].clone(), full.clone()]
             names = ["act", "logp", "full"]
-            if dump:
-                win = dbg[:rows * 64].view(rows, 64)[:, :49].clone()
-                bad_in = (win != obs.reshape(rows, D)[:, :49]).any(1)
-                if bool(bad_in.any()):
-                    idx = bad_in.nonzero().flatten()
-                    print(var, "rep", k, "window != input in", int(idx.numel()), "rows, waves",
-                          sorted(set((idx // 64).tolist()))[:8], flush=True)
-                cur += [win, dbg[rows * 64:rows * 96].view(rows, 32).clone(),
-                        dbg[rows * 96:].view(rows, 8).clone()]
-                names += ["window", "layernorm", "heads"]
             if ref is None:
                 ref = cur
                 continue
@@ -97,18 +107,16 @@ def main():
                 if not torch.equal(x, y):
                     d = (x != y).nonzero()
                     nd += 1
-                    rr = d[:, 0] * (n if name in ("act", "logp") else 1)
-                    if name in ("act", "logp"):
-                        rr = d[:, 0] * n + d[:, 1]
-                    if name == "full":
-                        rr = d[:, 0] * n + d[:, 1]
+                    rr = d[:, 0] * n + d[:, 1]   # (env, ship) -> row
                     waves |= set((rr // 64).tolist())
+                    lanes |= set((rr % 64).tolist())
                     if nd <= 6:
                         print(var, "rep", k, name, int((x != y).sum()), "differ, max |d|",
                               float((x - y).abs().max()), "rows", sorted(set(rr.tolist()))[:6],
                               "waves", sorted(set((rr // 64).tolist()))[:6], flush=True)
         print(var, "mismatching (rep, output) pairs:", nd, "of", len(ref) * (reps - 1),
-              "waves involved:", len(waves), sorted(waves)[:10], flush=True)
+              "waves involved:", len(waves), sorted(waves)[:10],
+              "lanes:", (min(lanes), max(lanes)) if lanes else None, flush=True)
 
 
 if __name__ == "__main__":
