@@ -465,13 +465,43 @@ __device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const float *xt,
 // A wave's rows up to the fc1 tile: conv head + LayerNorm (one row per lane),
 // the observation copy for the rollout buffer, and the LayerNorm outputs into
 // the wave's fc1 input tile in LDS (xt) for mlp_heads.
+#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12
+// Diagnostics probe 12: the first head of every wave (all heads at once) saves
+// each stage of its rows here; the partner's second head, run while the other
+// wave of its SIMD runs its MLP, compares stage by stage (window loads, pooled
+// conv1 maps in LDS, conv head outputs, LayerNorm tail loads, LayerNorm
+// outputs) and counts rows that differ per stage and lane (lnw_probe_counts).
+constexpr int PROBE_ROWS = 131072, PROBE_W = 256;
+__device__ float probe_buf[(size_t)PROBE_ROWS * PROBE_W];
+__device__ unsigned probe_cnt[5 * 64];
+template <int N>
+__device__ __forceinline__ void probe_stage(int cmp, int stage, long long row, int off, const float (&v)[N],
+                                            int lane) {
+  if (row >= PROBE_ROWS) return;
+  float *b = probe_buf + (size_t)row * PROBE_W + off;
+  if (!cmp) {
+#pragma unroll
+    for (int k = 0; k < N; k++) b[k] = v[k];
+    return;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < N; k++) bad = bad || __float_as_uint(b[k]) != __float_as_uint(v[k]);
+  if (bad) atomicAdd(&probe_cnt[stage * 64 + lane], 1u);
+}
+#define PROBE_STAGE(st, off, v) probe_stage(probe_cmp, st, r0 + (threadIdx.x & ~(WAVE - 1)) + lane, off, v, lane)
+#else
+#define PROBE_STAGE(st, off, v) ((void)0)
+#endif
+
 template <int NI>
 __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *P, float *warea, int lane,
                                              bool valid, long long e, int i, long long istride, long long r0,
-                                             long long rows) {
+                                             long long rows, int probe_cmp = 0) {
   constexpr int KS = NI + 4;
   const lnw_policy_args &a = pa.a;
   const int n = a.n, D = a.D, n_in = pa.n_in;
+  (void)probe_cmp;
   // ---- conv head + LayerNorm, one row per lane -------------------------------
   // The row's window and LayerNorm tail are loaded once, every load issued
   // together, into registers (the tail's loads were one dependent round trip
@@ -487,13 +517,24 @@ __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *
 #ifdef LNW_PROBE_NOCONV  // timing probes only (tools/policy_probe.py): no conv head
       for (int k = 0; k < 12; k++) h[k] = win[k];
 #else
+      PROBE_STAGE(0, 0, win);
       conv_head_win(P, win, warea + lane, WAVE, a.bn_running != 0, h);
+#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12
+      {
+        float pm[45];
+        for (int k = 0; k < 45; k++) pm[k] = warea[lane + k * WAVE];
+        PROBE_STAGE(1, 49, pm);
+      }
+#endif
+      PROBE_STAGE(2, 94, h);
 #endif
     }
     // the tail after the head (its registers are the head's), one batch of loads
     float tl[NI - 12];
     load_tail(a.obs + e * istride + (long long)i * D, D, tl);
+    PROBE_STAGE(3, 106, tl);
     layer_norm_tail<NI>(P, tl, n_in, h, u);
+    PROBE_STAGE(4, 170, u);
   } else {
 #pragma unroll
     for (int k = 0; k < NI; k++) u[k] = 0.f;
@@ -506,6 +547,9 @@ __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *
   // (in place: lnw_observe_ex wrote the rows into the rollout buffer itself;
   // only the rows of envs whose episode ended are zeroed)
   const bool in_place = a.obs_out == a.obs && a.obs_env_stride == istride;
+#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12
+  if (probe_cmp) return;
+#endif
   if (a.obs_out && (!in_place || a.live)) {
     const int D4 = D >> 2;
     const long long rw = r0 + (threadIdx.x & ~(WAVE - 1));
@@ -536,9 +580,12 @@ __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *
 // runs its MLP (1 VALU FMA chains, 2 LDS reads of its own tile, 3 global
 // loads, 4 s_sleep, 5 MFMA chains on registers, 6 LDS writes past its tile,
 // 7 global stores to its rows' log-prob outputs (rewritten after), 8 v_exp /
-// v_log / v_rcp / v_sqrt chains, 9 integer hashing); nothing it computes is kept.
+// v_log / v_rcp / v_sqrt chains, 9 integer hashing; 10, in head_and_mlp: its
+// own head again, rewriting the same tile; 11 its tile rows read and written
+// back unchanged; 12 its head again, compared stage by stage, probe_stage);
+// nothing it computes is kept.
 template <int MODE, int KS>
-__device__ __noinline__ void disturb(const PolicyArgs &pa, float *warea, int lane, long long e, int i) {
+__device__ __forceinline__ void disturb(const PolicyArgs &pa, float *warea, int lane, long long e, int i) {
   float acc0 = (float)lane, acc1 = 1.f, acc2 = 2.f, acc3 = 3.f;
   if (MODE == 1) {
     for (int it = 0; it < 2000; it++) {
@@ -573,6 +620,19 @@ __device__ __noinline__ void disturb(const PolicyArgs &pa, float *warea, int lan
     for (int it = 0; it < 500; it++) {
       acc0 = __builtin_amdgcn_exp2f(acc0 * 1e-3f); acc1 = __builtin_amdgcn_logf(acc1 + 1.f);
       acc2 = __builtin_amdgcn_rcpf(acc2 + 1.f); acc3 = __builtin_amdgcn_sqrtf(acc3 + 1.f);
+    }
+  } else if (MODE == 11) {  // its own tile row read and written back, unchanged
+    float *row = warea + lane * KS;
+    for (int it = 0; it < 60; it++) {
+      f32x4v v[KS / 4 - 1];
+#pragma unroll
+      for (int k4 = 0; k4 < KS / 4 - 1; k4++) {
+        v[k4] = *(const f32x4v *)(row + 4 * k4);
+        asm volatile("" : "+v"(v[k4]));  // (not a load-store pair the compiler may drop)
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < KS / 4 - 1; k4++) *(f32x4v *)(row + 4 * k4) = v[k4];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   } else if (MODE == 9) {
     unsigned h0 = (unsigned)lane, h1 = 7u;
@@ -628,7 +688,11 @@ __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *
     }
     for (int ph = 0; ph < nph; ph++) {
       if (ph == rank) mlp_heads<Q1>(pa, warea, lane, g, m, mean, lsd);
-#ifdef LNW_PROBE_DISTURB  // diagnostics probes only (tools/build_probes.sh): the partner's work
+#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 10  // probes: the partner redoes its head (same tile)
+      else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
+#elif defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12  // probes: ... comparing every stage
+      else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows, 1);
+#elif defined(LNW_PROBE_DISTURB)  // diagnostics probes only (tools/build_probes.sh): the partner's work
       else disturb<LNW_PROBE_DISTURB, NI + 4>(pa, warea, lane, e, i);
 #endif
       __syncthreads();
@@ -969,6 +1033,15 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
     policy_act_kernel<MAX_IN><<<blocks, PA_THREADS, lds, (hipStream_t)stream>>>(pa);
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
+
+#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12
+// probe 12's counters [stage][lane] since the last call (then zeroed)
+int lnw_probe_counts(unsigned *host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(probe_cnt), sizeof(probe_cnt)) != hipSuccess) return LNW_EDEVICE;
+  static const unsigned zero[5 * 64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(probe_cnt), zero, sizeof(zero)) == hipSuccess ? 0 : LNW_EDEVICE;
+}
+#endif
 
 // Packed critic: see rollout_post_kernel (BatchedCritic.packed()).
 int lnw_rollout_post(const lnw_rollout_post_args *args, void *stream) {

@@ -59,6 +59,9 @@ struct KParams {
   // steps' action arrays / row kinds / outputs (0: every step uses the same)
   int seq_steps;
   long long seq_act, seq_kind, seq_obs[2], seq_rew[2], seq_done, seq_cog;
+  // (lnw_step_seq) the sequence's base pointers: actions, row kinds, obs blue / red,
+  // rewards blue / red, done, cog
+  void *seq_ptr[8];
   int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table, bit13 4-ship phase-S rows stored row by row instead of line-aligned, bit15 the group kernel's fire loop entry by entry
 };
 

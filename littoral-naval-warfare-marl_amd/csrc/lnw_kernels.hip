@@ -2192,6 +2192,13 @@ __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, C
   wave_lds_sync();
   for (int g0 = 0; g0 < nenv; g0 += EPG) {
     const int ne = (nenv - g0) < EPG ? (nenv - g0) : EPG;
+    // every window load of this pass landed before the rows are built: with
+    // the compiler's partial vmcnt waits here (the loads issued before the
+    // previous pass's stores) rows of the contact variant's phase O came out
+    // with float4s of their window record stale, in about one 45-step
+    // 4 096-env run in four, never with this wait ("Phase O's
+    // window loads"); it costs the melee step ~1.5 %
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (my_e < ne && !(P.dbg_skip & 8))
       row_regs_t<NB>(c, duct_col, g0 + my_e, my_k, own0, v, w48, row, xg);
     wave_lds_sync();
@@ -3306,7 +3313,14 @@ __device__ __forceinline__ void step_body(
         }
         __syncthreads();
         if (wid == 1) {
+#ifdef LNW_PSPLIT_STAY  // diagnostics: wave 1 stays resident through wave 0's phase O
+          if (phase_o) {
+            __syncthreads();  // wave 0's phase-O barrier
+            __syncthreads();  // the end of phase O
+          }
+#else
           if (SEQ && phase_o) __syncthreads();  // wave 0's phase-O barrier
+#endif
           return;
         }
         {
@@ -3455,6 +3469,9 @@ __device__ __forceinline__ void step_body(
   // ---- phase O: observations ---------------------------------------------
   if constexpr (ST) write_obs_t<NB, NR>(P, S, c, duct_col, obs_b, obs_r, env0, nenv);
   else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
+#ifdef LNW_PSPLIT_STAY
+  if (psplit) __syncthreads();
+#endif
 }
 
 // One step (SEQ = false: lnw_step), or P.seq_steps steps in one launch
@@ -3473,16 +3490,34 @@ __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 
     step_body<NB, NR, CW, REFW, UN, PS, false>(P, S, actions, row_kind, obs_b, obs_r, rew_b, rew_r, done_out,
                                                cog_out);
   } else {
-    const long long asz = P.act_dtype == LNW_ACT_F64 ? 8 : 4, rsz = P.rew_f64 ? 8 : 4;
-    for (int k = 0; k < P.seq_steps; k++) {
-      auto adv = [&](void *p, long long stride, long long sz) {
-        return p ? (void *)((char *)p + (long long)k * stride * sz) : nullptr;
+    typedef const __attribute__((address_space(4))) char *KAp;
+    typedef const __attribute__((address_space(4))) KParams *KPp;
+    typedef const __attribute__((address_space(4))) KState *KSp;
+    // the kernarg segment: P at offset 0, S after it at its alignment (the
+    // AMDGPU kernel ABI lays the arguments out in order, each at its alignment)
+    constexpr size_t S_OFF = (sizeof(KParams) + alignof(KState) - 1) / alignof(KState) * alignof(KState);
+    for (int k = 0;; k++) {
+      // the kernel arguments read afresh every step (through an opaque copy of
+      // the kernarg segment pointer; not &P, which would make the compiler copy
+      // the arguments to scratch), the sequence's pointers among them (seq_ptr):
+      // otherwise everything the step derives from them is hoisted out of the
+      // loop and held live across it, and the body spills
+      KAp ka = (KAp)__builtin_amdgcn_kernarg_segment_ptr();
+      asm volatile("" : "+s"(ka));
+      KPp pp = (KPp)ka;
+      KSp sp = (KSp)(ka + S_OFF);
+      const KParams &Pk = *(const KParams *)pp;
+      if (k >= Pk.seq_steps) break;
+      const long long asz = Pk.act_dtype == LNW_ACT_F64 ? 8 : 4, rsz = Pk.rew_f64 ? 8 : 4;
+      auto adv = [&](int j, long long stride, long long sz) {
+        char *p = (char *)Pk.seq_ptr[j];
+        return p ? (void *)(p + (long long)k * stride * sz) : nullptr;
       };
       step_body<NB, NR, CW, REFW, UN, PS, true>(
-          P, S, adv(actions, P.seq_act, asz), (const uint8_t *)adv((void *)row_kind, P.seq_kind, 1),
-          (float *)adv(obs_b, P.seq_obs[0], 4), (float *)adv(obs_r, P.seq_obs[1], 4),
-          (float *)adv(rew_b, P.seq_rew[0], rsz), (float *)adv(rew_r, P.seq_rew[1], rsz),
-          (int32_t *)adv(done_out, P.seq_done, 4), (float *)adv(cog_out, P.seq_cog, rsz));
+          Pk, *(const KState *)sp, adv(0, Pk.seq_act, asz), (const uint8_t *)adv(1, Pk.seq_kind, 1),
+          (float *)adv(2, Pk.seq_obs[0], 4), (float *)adv(3, Pk.seq_obs[1], 4),
+          (float *)adv(4, Pk.seq_rew[0], rsz), (float *)adv(5, Pk.seq_rew[1], rsz),
+          (int32_t *)adv(6, Pk.seq_done, 4), (float *)adv(7, Pk.seq_cog, rsz));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's state stores done
       __syncthreads();
     }
@@ -3919,6 +3954,7 @@ struct lnw_handle {
   bool no_split_rows = false;  // LNW_NO_SPLIT_ROWS (A/B): row-writing contact steps keep phase S on one wave
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
+  bool seq_fused = false;  // LNW_SEQ_FUSED: lnw_step_seq's one-launch sequence kernels
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
   int last_kernel = LNW_KERNEL_NONE;     // lnw_step_kernel: what the last lnw_step launched
   bool has_medium = false;               // the spawn spec has medium ships (runtime-size kernels only)
@@ -4264,7 +4300,9 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->no_split_rows = getenv("LNW_NO_SPLIT_ROWS") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
-  // LNW_NO_XCD_REMAP: workgroup b steps env chunk b (A/B tests of xcd_chunk)
+  // LNW_SEQ_FUSED (A/B): lnw_step_seq through the sequence kernels (one launch
+  // for the K steps) instead of K lnw_step launches; measured slower
+  h->seq_fused = getenv("LNW_SEQ_FUSED") != nullptr;
   h->kp.xcd_remap = getenv("LNW_NO_XCD_REMAP") == nullptr ? 1 : 0;
   // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
   // terrain mask instead of loading LOS-table words (A/B)
@@ -4583,6 +4621,9 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
     k.seq_rew[1] = seq->rew_red_step;
     k.seq_done = seq->done_step;
     k.seq_cog = seq->cog_step;
+    void *const ptrs[8] = {actions_dev, (void *)row_kind_dev, obs_blue_dev, obs_red_dev,
+                           rew_blue_dev, rew_red_dev, done_dev, cog_dev};
+    for (int j = 0; j < 8; j++) k.seq_ptr[j] = ptrs[j];
   }
   KState s = make_state(h);
   size_t lds = step_launch_lds_bytes(h, k.epw);
@@ -4599,7 +4640,7 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
                      k.los_mode == 0 && h->E % (EPW * UNITS) == 0 && !(h->dbg_skip & (1 | 2 | 512));
   // lnw_step_seq's fused kernels: the units kernel and the templated 4v4 default variant
   const bool seq_fused = units || (templated && h->nb == 4 && !h->contact && k.los_mode != 2);
-  if (seq && (!seq_fused || h->prof)) return STEP_NOT_FUSED;
+  if (seq && (!seq_fused || h->prof || !h->seq_fused)) return STEP_NOT_FUSED;
   // per-unit records (LNW_PROF) of the kernel launched below (the group kernel has its own grid)
   const unsigned nwg = use_group ? (unsigned)((h->E + GEPW - 1) / GEPW) : grid.x;
   if (h->prof) {

@@ -1,8 +1,8 @@
 """lnw_step_seq (BatchedGame.step_seq): K steps of an action sequence known
 ahead of time in one call. Its results must be those of K lnw_step calls — the
-fused sequence kernels (the units kernel and the templated 4v4 default variant,
-where each workgroup moves through the K steps on its own) and the K-launch
-fallback of every other shape alike: every step's observations, rewards, done
+K launches it makes by default and, under LNW_SEQ_FUSED, the one-launch
+sequence kernels (the units kernel and the templated 4v4 default variant, where
+each workgroup moves through the K steps on its own) alike: every step's observations, rewards, done
 and cog, the action rows as each step left them (an untrained red's salvo
 write-back, game.py:375-379) and the whole state afterwards, bit for bit. The
 workloads cross the 40-step horizon's in-kernel auto-reset and mix quiet and
@@ -65,9 +65,14 @@ def _same(x, y):
     return torch.equal(x, y)
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_step_seq_equals_steps(name):
+def test_step_seq_equals_steps(name, fused, monkeypatch):
     from lnw import _abi
+    if fused:  # the one-launch sequence kernels (LNW_SEQ_FUSED, read at lnw_create)
+        monkeypatch.setenv("LNW_SEQ_FUSED", "1")
+    else:
+        monkeypatch.delenv("LNW_SEQ_FUSED", raising=False)
     cs = CASES[name]
     grid = _oracle.load_fixture("grids.npz")["grid100"]
     E, nb, K = cs["E"], cs["nb"], 45
@@ -106,13 +111,14 @@ def test_step_seq_equals_steps(name):
         g.close()
 
 
-def test_step_seq_vs_oracle_shard():
+def test_step_seq_vs_oracle_shard(monkeypatch):
     """The fused sequence at config 3's per-GPU shard (8 192 envs, quiet direct
     mode, mixed quiet / fighting workgroups) against the CPU oracle directly:
     45 steps in one launch, per (step, env) observation hashes, done, rewards
     and cog (orc_fullsize_range)."""
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
+    monkeypatch.setenv("LNW_SEQ_FUSED", "1")
     grid = _oracle.load_fixture("grids.npz")["grid100"]
     E, S, seed = 8192, 45, 313
     pos = np.array([REF_SPAWNS] * E, np.int32)

@@ -10,7 +10,9 @@
 // lgkmcnt(0), the control), then checks its row; every odd wave keeps the LDS
 // busy with b128 reads and writes of its own area (partner 0) or runs
 // v_mfma_f32_16x16x32_bf16 chains on registers (partner 1). Mismatches are
-// counted per lane. usage: ds_hazard_probe [iters] [partner]
+// counted per lane. Mode 3: the data VGPRs written by v_mov right before the
+// ds_write_b128 (a read-after-write the hardware interlocks).
+// usage: ds_hazard_probe [iters] [partner]
 //   hipcc --offload-arch=gfx950 -O3 tools/ds_hazard_probe.hip -o tools/ds_hazard_probe
 #include <hip/hip_runtime.h>
 
@@ -63,8 +65,14 @@ __global__ __launch_bounds__(512, 1) void probe(int iters, int partner, int *bad
         asm volatile(PROBE_SETUP "v_mov_b32 v100, -1\n\tv_mov_b32 v101, -1\n\ts_waitcnt lgkmcnt(0)"
                      :: "v"(want.x), "v"(want.y), "v"(want.z), "v"(want.w), "v"(addr)
                      : "v100", "v101", "v102", "v103", "v104", "memory");
-      else
+      else if (MODE == 2)
         asm volatile(PROBE_SETUP "v_mov_b32 v104, 0\n\ts_waitcnt lgkmcnt(0)"
+                     :: "v"(want.x), "v"(want.y), "v"(want.z), "v"(want.w), "v"(addr)
+                     : "v100", "v101", "v102", "v103", "v104", "memory");
+      else  // mode 3: the data written by VALU right before the write (no wait states between)
+        asm volatile("v_mov_b32 v104, %4\n\ts_nop 4\n\t"
+                     "v_mov_b32 v100, %0\n\tv_mov_b32 v101, %1\n\tv_mov_b32 v102, %2\n\tv_mov_b32 v103, %3\n\t"
+                     "ds_write_b128 v104, v[100:103]\n\ts_waitcnt lgkmcnt(0)"
                      :: "v"(want.x), "v"(want.y), "v"(want.z), "v"(want.w), "v"(addr)
                      : "v100", "v101", "v102", "v103", "v104", "memory");
       const i32x4 got = mine[0];
@@ -78,19 +86,21 @@ int main(int argc, char **argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 2000;
   const int partner = argc > 2 ? atoi(argv[2]) : 0;
   int *bad, *sink;
-  hipMalloc(&bad, 3 * 64 * sizeof(int));
+  hipMalloc(&bad, 4 * 64 * sizeof(int));
   hipMalloc(&sink, 512 * sizeof(int));
-  hipMemset(bad, 0, 3 * 64 * sizeof(int));
+  hipMemset(bad, 0, 4 * 64 * sizeof(int));
   const size_t lds = 8 * 64 * 4 * sizeof(i32x4);  // 32 KB per block
   const int blocks = 1024;                          // 4 per CU
   probe<0><<<blocks, 512, lds>>>(iters, partner, bad, sink);
   probe<1><<<blocks, 512, lds>>>(iters, partner, bad + 64, sink);
   probe<2><<<blocks, 512, lds>>>(iters, partner, bad + 128, sink);
+  probe<3><<<blocks, 512, lds>>>(iters, partner, bad + 192, sink);
   if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
-  std::vector<int> h(192);
-  hipMemcpy(h.data(), bad, 192 * sizeof(int), hipMemcpyDeviceToHost);
-  const char *names[3] = {"wait before overwrite (control)", "data overwritten next", "address overwritten next"};
-  for (int m = 0; m < 3; m++) {
+  std::vector<int> h(256);
+  hipMemcpy(h.data(), bad, 256 * sizeof(int), hipMemcpyDeviceToHost);
+  const char *names[4] = {"wait before overwrite (control)", "data overwritten next", "address overwritten next",
+                          "data written by VALU just before"};
+  for (int m = 0; m < 4; m++) {
     long long tot = 0;
     int lo = 64, hi = -1;
     for (int l = 0; l < 64; l++) {

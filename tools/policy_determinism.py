@@ -114,6 +114,17 @@ def main():
                         print(var, "rep", k, name, int((x != y).sum()), "differ, max |d|",
                               float((x - y).abs().max()), "rows", sorted(set(rr.tolist()))[:6],
                               "waves", sorted(set((rr // 64).tolist()))[:6], flush=True)
+        if hasattr(L, "lnw_probe_counts"):  # probe 12: rows whose second head differed, per stage
+            cnt = (C.c_uint * 320)()
+            L.lnw_probe_counts(cnt)
+            for st, name in enumerate(["window loads", "pooled conv1 maps (LDS)", "conv head out",
+                                       "LayerNorm tail loads", "LayerNorm out"]):
+                c = list(cnt[st * 64:(st + 1) * 64])
+                if sum(c):
+                    ln = [l for l in range(64) if c[l]]
+                    print(var, "probe stage", name, ":", sum(c), "rows, lanes", ln[0], "..", ln[-1], flush=True)
+                else:
+                    print(var, "probe stage", name, ": 0 rows", flush=True)
         print(var, "mismatching (rep, output) pairs:", nd, "of", len(ref) * (reps - 1),
               "waves involved:", len(waves), sorted(waves)[:10],
               "lanes:", (min(lanes), max(lanes)) if lanes else None, flush=True)
