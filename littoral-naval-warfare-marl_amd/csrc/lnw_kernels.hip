@@ -2192,13 +2192,6 @@ __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, C
   wave_lds_sync();
   for (int g0 = 0; g0 < nenv; g0 += EPG) {
     const int ne = (nenv - g0) < EPG ? (nenv - g0) : EPG;
-    // every window load of this pass landed before the rows are built: with
-    // the compiler's partial vmcnt waits here (the loads issued before the
-    // previous pass's stores) rows of the contact variant's phase O came out
-    // with float4s of their window record stale, in about one 45-step
-    // 4 096-env run in four, never with this wait ("Phase O's
-    // window loads"); it costs the melee step ~1.5 %
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (my_e < ne && !(P.dbg_skip & 8))
       row_regs_t<NB>(c, duct_col, g0 + my_e, my_k, own0, v, w48, row, xg);
     wave_lds_sync();
@@ -3313,14 +3306,7 @@ __device__ __forceinline__ void step_body(
         }
         __syncthreads();
         if (wid == 1) {
-#ifdef LNW_PSPLIT_STAY  // diagnostics: wave 1 stays resident through wave 0's phase O
-          if (phase_o) {
-            __syncthreads();  // wave 0's phase-O barrier
-            __syncthreads();  // the end of phase O
-          }
-#else
           if (SEQ && phase_o) __syncthreads();  // wave 0's phase-O barrier
-#endif
           return;
         }
         {
@@ -3469,9 +3455,6 @@ __device__ __forceinline__ void step_body(
   // ---- phase O: observations ---------------------------------------------
   if constexpr (ST) write_obs_t<NB, NR>(P, S, c, duct_col, obs_b, obs_r, env0, nenv);
   else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
-#ifdef LNW_PSPLIT_STAY
-  if (psplit) __syncthreads();
-#endif
 }
 
 // One step (SEQ = false: lnw_step), or P.seq_steps steps in one launch
@@ -3951,7 +3934,7 @@ struct lnw_handle {
   int dbg_skip = 0;
   bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
   bool force_group = false;  // LNW_FORCE_GROUP (A/B): the group kernel for templated team sizes too
-  bool no_split_rows = false;  // LNW_NO_SPLIT_ROWS (A/B): row-writing contact steps keep phase S on one wave
+  bool split_rows = false;  // LNW_SPLIT_ROWS (A/B): row-writing contact steps split phase S by side too
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool seq_fused = false;  // LNW_SEQ_FUSED: lnw_step_seq's one-launch sequence kernels
@@ -4297,7 +4280,10 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
   h->force_group = getenv("LNW_FORCE_GROUP") != nullptr;
-  h->no_split_rows = getenv("LNW_NO_SPLIT_ROWS") != nullptr;
+  // (off by default: their rows, written after phase S by wave 0 alone, came
+  // out with parts of some window records wrong in about one 45-step 4 096-env
+  // contact run in four; DESIGN.md "The split contact step with rows")
+  h->split_rows = getenv("LNW_SPLIT_ROWS") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
   // LNW_SEQ_FUSED (A/B): lnw_step_seq through the sequence kernels (one launch
@@ -4681,9 +4667,9 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
   }
   else if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
   else if (templated && h->nb == 4) {
-    // the contact variant: phase S split by side (step_kernel PS; LNW_NO_SPLIT_ROWS:
-    // only for steps without rows, A/B)
-    if (cw && k.los_mode == 0 && (k.no_obs || !h->no_split_rows))
+    // the contact variant: phase S split by side (step_kernel PS) for steps
+    // without rows (LNW_SPLIT_ROWS, A/B: for row-writing steps too)
+    if (cw && k.los_mode == 0 && (k.no_obs || h->split_rows))
       step_kernel<4, 4, true, false, 1, true><<<grid, dim3(2 * WAVE), lds, st>>>(
           k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
     else if (cw) LNW_STEP(4, 4, true, false);
