@@ -2200,6 +2200,12 @@ __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, C
       copy_side_t<NB, EPG * NB * (4 * NB + 52) / 4>(stage_b, obs_b, S.dummy, ne, env0 + g0, P.store_wt);
       copy_side_t<NR, EPG * NR * (4 * NR + 52) / 4>(stage_r, obs_r, S.dummy, ne, env0 + g0, P.store_wt);
     }
+    // this pass's stores complete before the next pass reuses their data
+    // registers (and before the wave ends after the last pass): without it the
+    // split contact step's rows came out with float4s of other rows in about
+    // one 45-step 4 096-env run in four ("The split contact step
+    // with rows"); 0 in 28 with it, at ~3 us of a 177 us melee step
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_lds_sync();
   }
 }
@@ -3934,7 +3940,7 @@ struct lnw_handle {
   int dbg_skip = 0;
   bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
   bool force_group = false;  // LNW_FORCE_GROUP (A/B): the group kernel for templated team sizes too
-  bool split_rows = false;  // LNW_SPLIT_ROWS (A/B): row-writing contact steps split phase S by side too
+  bool no_split_rows = false;  // LNW_NO_SPLIT_ROWS (A/B): row-writing contact steps keep phase S on one wave
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
   bool seq_fused = false;  // LNW_SEQ_FUSED: lnw_step_seq's one-launch sequence kernels
@@ -4280,10 +4286,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // LNW_NO_GROUP: runtime team sizes on the one-lane-per-env kernel (A/B tests)
   h->no_group = getenv("LNW_NO_GROUP") != nullptr;
   h->force_group = getenv("LNW_FORCE_GROUP") != nullptr;
-  // (off by default: their rows, written after phase S by wave 0 alone, came
-  // out with parts of some window records wrong in about one 45-step 4 096-env
-  // contact run in four; DESIGN.md "The split contact step with rows")
-  h->split_rows = getenv("LNW_SPLIT_ROWS") != nullptr;
+  h->no_split_rows = getenv("LNW_NO_SPLIT_ROWS") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
   // LNW_SEQ_FUSED (A/B): lnw_step_seq through the sequence kernels (one launch
@@ -4667,9 +4670,9 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
   }
   else if (k.los_mode == 2) LNW_STEP(0, 0, false, true);  // diagnostics: the reference's LOS work
   else if (templated && h->nb == 4) {
-    // the contact variant: phase S split by side (step_kernel PS) for steps
-    // without rows (LNW_SPLIT_ROWS, A/B: for row-writing steps too)
-    if (cw && k.los_mode == 0 && (k.no_obs || h->split_rows))
+    // the contact variant: phase S split by side (step_kernel PS; LNW_NO_SPLIT_ROWS:
+    // only for steps without rows, A/B)
+    if (cw && k.los_mode == 0 && (k.no_obs || !h->no_split_rows))
       step_kernel<4, 4, true, false, 1, true><<<grid, dim3(2 * WAVE), lds, st>>>(
           k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
     else if (cw) LNW_STEP(4, 4, true, false);

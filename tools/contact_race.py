@@ -48,6 +48,12 @@ def main():
     first = None
     good_rows = None
     for r in range(R):
+        # RACE_REF_NOSPLIT=1: run 0 on the emission path (LNW_NO_SPLIT_ROWS), the reference rows
+        if os.environ.get("RACE_REF_NOSPLIT"):
+            if r == 0:
+                os.environ["LNW_NO_SPLIT_ROWS"] = "1"
+            else:
+                os.environ.pop("LNW_NO_SPLIT_ROWS", None)
         sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40)
         g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grid, seed=seed)
         g.set_variant(variant)
