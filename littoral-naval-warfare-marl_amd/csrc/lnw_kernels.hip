@@ -2039,6 +2039,9 @@ __device__ __forceinline__ void write_obs(const KParams &P, const KState &S, Col
       copy_side(stage_b, obs_b, nb, side_D(P, 0), ne, env0 + g0, P.obs_stride[0]);
       copy_side(stage_r, obs_r, nr, side_D(P, 1), ne, env0 + g0, P.obs_stride[1]);
     }
+    // (as write_obs_t: the pass's stores complete before the next pass or the
+    // end of the wave reuses their registers)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_lds_sync();
   }
 }

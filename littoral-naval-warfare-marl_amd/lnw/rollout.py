@@ -409,16 +409,24 @@ class Rollout:
             return self._run_hip(forced_actions, on_step)
         return self._run_torch(generator, forced_actions, on_step)
 
-    def _buffers(self):
+    def _buffers(self, fill=True):
+        """The rollout's storage. fill=False (the HIP path): uninitialised, since
+        every element is written each step — the observe writes every ship's row
+        (a sunk ship's as zeros), the policy zeroes the rows, actions and
+        log-probabilities of envs whose episode ended and writes each env's
+        float32 flag, lnw_rollout_post writes every value, reward and running
+        flag (masked ones as zeros) — so the 1.4 GB observation buffer of a
+        32 768-env rollout is not zero-filled first (≈7 µs per step)."""
         g = self.g
         E, nb, A, D, T, dev = g.E, g.nb, g.A, g.Db, self.T, g.device
-        return dict(obs=torch.zeros((E, T, nb, D), dtype=torch.float32, device=dev),
-                    actions=torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev),
-                    log_probs=torch.zeros((E, T, nb, 4), dtype=torch.float32, device=dev),
-                    rewards=torch.zeros((E, T, nb), dtype=torch.float64, device=dev),
-                    values=torch.zeros((E, T), dtype=torch.float32, device=dev),
-                    running=torch.ones((E, T), dtype=torch.bool, device=dev),
-                    f32_step=torch.zeros((E, T), dtype=torch.bool, device=dev))
+        z = torch.zeros if fill else torch.empty
+        return dict(obs=z((E, T, nb, D), dtype=torch.float32, device=dev),
+                    actions=z((E, T, nb, 4), dtype=torch.float32, device=dev),
+                    log_probs=z((E, T, nb, 4), dtype=torch.float32, device=dev),
+                    rewards=z((E, T, nb), dtype=torch.float64, device=dev),
+                    values=z((E, T), dtype=torch.float32, device=dev),
+                    running=(torch.ones if fill else torch.empty)((E, T), dtype=torch.bool, device=dev),
+                    f32_step=z((E, T), dtype=torch.bool, device=dev))
 
     def _run_hip(self, forced_actions, on_step):
         import ctypes as C
@@ -428,7 +436,7 @@ class Rollout:
         g = self.g
         E, nb, nr, A, Db, Dr, T = g.E, g.nb, g.nr, g.A, g.Db, g.Dr, self.T
         dev = g.device
-        b = self._buffers()
+        b = self._buffers(fill=False)
         obs, acts, logp, rew, val, running, f32s = (b[k] for k in ("obs", "actions", "log_probs", "rewards",
                                                                 "values", "running", "f32_step"))
         full = torch.zeros((E, A, 4), dtype=torch.float64, device=dev)
