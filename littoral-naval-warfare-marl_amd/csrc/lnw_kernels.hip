@@ -2434,6 +2434,20 @@ __device__ __forceinline__ void emit_rows_al4_t(const KParams &P, const KState &
 // published progress > a (LDS counter, -1 until phase S starts: the emission
 // stage aliases the terrain mask phase M reads). Its stores count on its own
 // vmcnt, so wave 0's loads in phase S never wait behind observation stores.
+//
+// The pair's contract (publish_progress / wait_progress): it orders LDS only.
+// publish_progress(v) drains the publishing wave's LDS operations
+// (s_waitcnt lgkmcnt(0)) and then stores v; a wave that has read a count >= v
+// sees every LDS write the publisher made before it (a completed LDS write is
+// visible to every wave of the CU, and the reader's later LDS reads are issued
+// after its load of the count returned). It gives no ordering for global
+// memory (no vmcnt wait, no release/acquire fence), and none the other way:
+// the publisher may overwrite any LDS word the reader has not finished with.
+// So a reader may use only LDS data the publisher will not change again in
+// this step — the emission path reads agent a's columns, which phase S
+// finishes with agent a's turn. (Round 4's per-ship handoff broke the second
+// rule: wave 1 read columns and HBM target lists that wave 0's later turns
+// rewrite; it stays out.)
 __device__ inline int wait_progress(const int *prog, int want) {
   int v;
   while ((v = __hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < want)
