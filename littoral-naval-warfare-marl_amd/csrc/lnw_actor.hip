@@ -412,11 +412,18 @@ __device__ __forceinline__ void tanh_all(f32x4v (&acc)[4][NTO]) {
       for (int v = 0; v < 4; v++) acc[rt][nt][v] = tanh_fast(acc[rt][nt][v]);
 }
 
+// bf16x8 elements of the MLP's packed weights (three planes per layer: fc1
+// 4 x Q1/2, fc2 4 x 2, fc3 2 x 2, heads 1 x 1 tiles of WAVE, as mlp_heads reads them)
+template <int NI>
+__host__ __device__ constexpr int mlp_bf16x8() {
+  return 3 * (4 * (NI / 32) + 4 * 2 + 2 * 2 + 1 * 1) * WAVE;
+}
+
 // fc1 / fc2 / fc3 and both heads of the wave's 64 rows on the matrix cores
 // (xb: fc1's B operand), then each row's head outputs brought to its own lane
 template <int Q1>
-__device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const float *xt, int lane, int g, int m,
-                                          float (&mean)[NOUT], float (&lsd)[NOUT]) {
+__device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const bf16x8 *Fw, const float *xt, int lane,
+                                          int g, int m, float (&mean)[NOUT], float (&lsd)[NOUT]) {
   constexpr int KS = 16 * Q1 + 4;  // the tile's row stride (policy_act_kernel)
   const lnw_policy_args &a = pa.a;
   f32x4v xb[4][Q1];
@@ -425,7 +432,7 @@ __device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const float *xt,
 #pragma unroll
     for (int q = 0; q < Q1; q++) xb[rt][q] = *(const f32x4v *)(xt + (rt * 16 + m) * KS + 16 * q + 4 * g);
   // weights: three bf16 planes per layer (mfma_layer3), layers in order
-  const bf16x8 *Fw = (const bf16x8 *)(a.params + pa.off_w1);
+  // Fw: the three bf16 planes of every layer (global, or the block's LDS copy)
   constexpr int O2 = 3 * 4 * (Q1 / 2) * WAVE, O3 = O2 + 3 * 4 * 2 * WAVE, OH = O3 + 3 * 2 * 2 * WAVE;
   const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
   f32x4v h1[4][4];
@@ -665,7 +672,7 @@ __device__ __forceinline__ void disturb(const PolicyArgs &pa, float *warea, int 
 // SIMD of each wave comes from HW_ID, so nothing assumes how the hardware
 // deals waves to SIMDs; one MLP at a time per SIMD also holds for any dealing.
 template <int NI>
-__device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *P, float *warea, int lane, int g,
+__device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *P, const bf16x8 *Fw, float *warea, int lane, int g,
                                              int m, bool valid, long long e, int i, long long istride, long long r0,
                                              long long rows, float (&mean)[NOUT], float (&lsd)[NOUT]) {
   constexpr int Q1 = NI / 16;
@@ -687,7 +694,7 @@ __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *
       rank = w2 == wv ? r2 : rank;
     }
     for (int ph = 0; ph < nph; ph++) {
-      if (ph == rank) mlp_heads<Q1>(pa, warea, lane, g, m, mean, lsd);
+      if (ph == rank) mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
 #if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 10  // probes: the partner redoes its head (same tile)
       else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
 #elif defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12  // probes: ... comparing every stage
@@ -698,7 +705,7 @@ __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *
       __syncthreads();
     }
   } else {
-    mlp_heads<Q1>(pa, warea, lane, g, m, mean, lsd);
+    mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
   }
 }
 
@@ -715,6 +722,17 @@ __global__ __launch_bounds__(PA_THREADS, 512 / PA_THREADS) void policy_act_kerne
   constexpr int WAREA = (45 > KS ? 45 : KS) * WAVE;
   float *warea = actor_lds + ((n_par + 3) & ~3) + (threadIdx.x / WAVE) * WAREA;
   for (int i = threadIdx.x; i < n_par; i += blockDim.x) P[i] = a.params[i];
+  // the MLP's weights (three bf16 planes per layer, mlp_bf16x8<NI> of them):
+  // at NI = 32 a copy in LDS after the wave areas, loaded once per block while
+  // the heads run, so each wave's MFMA chains read their A operands from LDS
+  // instead of 51 KB apiece from L2 (at NI = 64 they do not fit beside the
+  // larger tiles and stay in global memory)
+  const bf16x8 *Fw = (const bf16x8 *)(a.params + pa.off_w1);
+  if constexpr (NI == 32) {
+    bf16x8 *wl = (bf16x8 *)(actor_lds + ((n_par + 3) & ~3) + (PA_THREADS / WAVE) * WAREA);
+    for (int i = threadIdx.x; i < mlp_bf16x8<NI>(); i += blockDim.x) wl[i] = Fw[i];
+    Fw = wl;
+  }
   const int n = a.n, D = a.D;
   const long long rows = a.E * n;
   const long long r0 = (long long)blockIdx.x * PA_THREADS;
@@ -759,7 +777,7 @@ __global__ __launch_bounds__(PA_THREADS, 512 / PA_THREADS) void policy_act_kerne
     lsd[v] = 0.f;
   }
 #else
-  head_and_mlp<NI>(pa, P, warea, lane, g, m, valid, e, i, istride, r0, rows, mean, lsd);
+  head_and_mlp<NI>(pa, P, Fw, warea, lane, g, m, valid, e, i, istride, r0, rows, mean, lsd);
 #endif
   if (!valid) return;
   // the row's env and ship again, from an opaque copy of the row index: so
@@ -1024,6 +1042,7 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   const unsigned blocks = (unsigned)((rows + PA_THREADS - 1) / PA_THREADS);
   const int npar4 = (CONV_PARAMS + 2 * pa.n_in + 3) & ~3;
   size_t lds = (size_t)(npar4 + (PA_THREADS / WAVE) * (pa.n_in <= 32 ? 45 : MAX_IN + 4) * WAVE) * sizeof(float);
+  if (pa.n_in <= 32) lds += (size_t)mlp_bf16x8<32>() * 16;  // the MLP weights' LDS copy
 #ifdef LNW_PROBE_ONEBLOCK  // probe builds: one block per CU
   if (lds < 84 * 1024) lds = 84 * 1024;
 #endif
