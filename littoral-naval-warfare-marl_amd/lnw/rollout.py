@@ -445,6 +445,8 @@ class Rollout:
         red_actor_rows = self.red != "script" and self.red_actor is not None
         ap = self.actor.packed_policy()
         cp = self.critic.packed(nb, Db) if self.critic is not None else None
+        if cp is None:  # (no critic: nothing writes the values, which are zeros)
+            val.zero_()
         rap = self.red_actor.packed_policy() if red_actor_rows else None
         fa = None
         if forced_actions is not None:

@@ -68,6 +68,36 @@ def test_rollout_buffers():
     g.close()
 
 
+def test_rollout_storage_fully_written():
+    """The HIP rollout allocates its storage uninitialised (every element is
+    written each step): a run into storage pre-filled with NaN garbage equals a
+    run into zeroed storage, and without a critic the values come out zero."""
+    from lnw.rollout import BatchedActor, BatchedCritic, Rollout
+    E, T = 320, 10
+    torch.manual_seed(4)
+    actor = BatchedActor.for_obs(68).cuda()
+    outs = []
+    for crit in (True, False):
+        for garbage in (False, True):
+            g = _game(E, seed=9)
+            torch.manual_seed(5)
+            critic = BatchedCritic(g.Db * g.nb).cuda() if crit else None
+            r = Rollout(g, actor, critic, steps=T, noise=0.05, seed=21)
+            if garbage:  # the caching allocator hands the next run blocks full of NaNs
+                junk = [torch.full((E * T * 4 * 68 * 2,), float("nan"), device="cuda") for _ in range(3)]
+                del junk
+            out = r.run()
+            torch.cuda.synchronize()
+            outs.append({k: v.clone() for k, v in out.items() if torch.is_tensor(v)})
+            g.close()
+    for a, b in ((outs[0], outs[1]), (outs[2], outs[3])):
+        for k in a:
+            assert torch.equal(a[k].view(torch.uint8), b[k].view(torch.uint8)), k
+    assert torch.equal(outs[2]["values"], torch.zeros_like(outs[2]["values"]))
+    for k in ("obs", "log_probs", "actions", "rewards"):
+        assert torch.isfinite(outs[1][k]).all() and torch.isfinite(outs[3][k]).all(), k
+
+
 def test_rollout_replays_with_stepped_actions():
     """Stepping a second game with the rollout's recorded actions reproduces the
     recorded observations (same seed, scripted red)."""
