@@ -663,50 +663,52 @@ __device__ __forceinline__ void disturb(const PolicyArgs &pa, float *warea, int 
 #endif
 
 // The phases of a block. PA_THREADS = 512 (one block per CU, two waves per
-// SIMD): every wave runs its head, then the waves of each SIMD run their MLPs
-// one at a time — a wave's MLP (v_mfma_f32_16x16x32_bf16 chains and the
-// ds_bpermute gather of the heads) while the other wave of its SIMD executed
-// anything at all came out nondeterministic in rows 48-63 (lanes 48-63: the
-// fourth 16-row tile) of one of the two waves (DESIGN.md "The policy reading
-// its rows in place"); with the partner parked at a barrier it is exact. The
-// SIMD of each wave comes from HW_ID, so nothing assumes how the hardware
-// deals waves to SIMDs; one MLP at a time per SIMD also holds for any dealing.
+// SIMD): every wave runs its head, a barrier, then every wave its MLP. A wave's
+// head (its conv, LayerNorm and fc1 tile) running while the other wave of its
+// SIMD ran its MLP (v_mfma_f32_16x16x32_bf16 chains) came out wrong in lanes
+// 48-63 of the head's wave ("The policy kernel's nondeterminism");
+// heads beside heads and MLPs beside MLPs are exact. (One block per CU: the
+// block's LDS is larger than half the CU's, so no other block's head shares a
+// SIMD with these MLPs.) The diagnostics probes keep round 5's schedule, the
+// waves of each SIMD taking their MLPs one at a time, to run their partner
+// workloads beside each MLP.
 template <int NI>
 __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *P, const bf16x8 *Fw, float *warea, int lane, int g,
                                              int m, bool valid, long long e, int i, long long istride, long long r0,
                                              long long rows, float (&mean)[NOUT], float (&lsd)[NOUT]) {
   constexpr int Q1 = NI / 16;
   head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
-  if constexpr (PA_THREADS > 256) {
-    constexpr int NWB = PA_THREADS / WAVE;
-    __shared__ int simd_of[NWB];
-    const int wv = (int)(threadIdx.x / WAVE);
-    const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3);  // hwreg(HW_ID).SIMD_ID
-    if (lane == 0) simd_of[wv] = simd;
-    __syncthreads();
-    int rank = 0, nph = 1;  // this wave's turn on its SIMD; turns needed by the busiest SIMD
+#ifndef LNW_PROBE_DISTURB
+  if constexpr (PA_THREADS > WAVE) __syncthreads();  // every head done before any MLP
+  mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
+#else
+  constexpr int NWB = PA_THREADS / WAVE;
+  __shared__ int simd_of[NWB];
+  const int wv = (int)(threadIdx.x / WAVE);
+  const int simd = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3);  // hwreg(HW_ID).SIMD_ID
+  if (lane == 0) simd_of[wv] = simd;
+  __syncthreads();
+  int rank = 0, nph = 1;  // this wave's turn on its SIMD; turns needed by the busiest SIMD
 #pragma unroll
-    for (int w2 = 0; w2 < NWB; w2++) {
-      int r2 = 0;
+  for (int w2 = 0; w2 < NWB; w2++) {
+    int r2 = 0;
 #pragma unroll
-      for (int w3 = 0; w3 < w2; w3++) r2 += simd_of[w3] == simd_of[w2] ? 1 : 0;
-      nph = r2 + 1 > nph ? r2 + 1 : nph;
-      rank = w2 == wv ? r2 : rank;
-    }
-    for (int ph = 0; ph < nph; ph++) {
-      if (ph == rank) mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
-#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 10  // probes: the partner redoes its head (same tile)
-      else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
-#elif defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12  // probes: ... comparing every stage
-      else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows, 1);
-#elif defined(LNW_PROBE_DISTURB)  // diagnostics probes only (tools/build_probes.sh): the partner's work
-      else disturb<LNW_PROBE_DISTURB, NI + 4>(pa, warea, lane, e, i);
-#endif
-      __syncthreads();
-    }
-  } else {
-    mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
+    for (int w3 = 0; w3 < w2; w3++) r2 += simd_of[w3] == simd_of[w2] ? 1 : 0;
+    nph = r2 + 1 > nph ? r2 + 1 : nph;
+    rank = w2 == wv ? r2 : rank;
   }
+  for (int ph = 0; ph < nph; ph++) {
+    if (ph == rank) mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
+#if LNW_PROBE_DISTURB == 10  // the partner redoes its head (same tile)
+    else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
+#elif LNW_PROBE_DISTURB == 12  // ... comparing every stage
+    else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows, 1);
+#else  // the partner's work (tools/build_probes.sh)
+    else disturb<LNW_PROBE_DISTURB, NI + 4>(pa, warea, lane, e, i);
+#endif
+    __syncthreads();
+  }
+#endif
 }
 
 template <int NI>
