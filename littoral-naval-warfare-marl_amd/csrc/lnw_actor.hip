@@ -279,7 +279,8 @@ __device__ __forceinline__ void keyed_eps(unsigned long long seed, unsigned long
   float u[8];
   philox_u8(seed, (slot << 38) + (unsigned long long)grow * 2ull, u);
 #pragma unroll
-  for (int c = 0; c < NOUT; c++) eps[c] = sqrtf(-2.0f * log1pf(-u[c])) * cosf(6.283185307179586f * u[4 + c]);
+  for (int c = 0; c < NOUT; c++)  // (v_cos_f32 takes revolutions: cos(2 pi u) without the range reduction)
+    eps[c] = sqrtf(-2.0f * log1pf(-u[c])) * __builtin_amdgcn_cosf(u[4 + c]);
 }
 
 // ---- the MLP on the matrix cores -------------------------------------------
