@@ -793,8 +793,10 @@ __global__ __launch_bounds__(PA_THREADS, 512 / PA_THREADS) void policy_act_kerne
   bool ok = true;
 #pragma unroll
   for (int o = 0; o < NOUT; o++) {
-    mean[o] = tanhf(mean[o]);
-    std_[o] = expf(lsd[o]);
+    // (the hardware exp2 / reciprocal forms: tanh_fast's absolute error < 3e-7,
+    // __expf's a few ulp; NaN, +-inf and overflow behave as tanhf / expf)
+    mean[o] = tanh_fast(mean[o]);
+    std_[o] = __expf(lsd[o]);
     ok = ok && !isnan(mean[o]) && !isnan(std_[o]);
   }
   // ---- sample / forced actions and log-probabilities -----------------------
