@@ -830,8 +830,11 @@ __global__ __launch_bounds__(PA_THREADS, 512 / PA_THREADS) void policy_act_kerne
 #pragma unroll
   for (int o = 0; o < NOUT; o++) {
     const float d = act[o] - mean[o];
-    const float var = std_[o] * std_[o];
-    lp[o] = -(d * d) / (2.0f * var) - logf(std_[o]) - 0.91893853320467274178f;
+    const float s = std_[o];
+    // log(std) is the log-scale itself wherever exp neither overflowed nor went to 0
+    // (the guarded rows carry std 1: log 0); v_rcp_f32 for 1 / var (1 ulp)
+    const float ls = (s > 0.f && s < INFINITY) ? ((a.forced || ok) ? lsd[o] : 0.f) : logf(s);
+    lp[o] = -(d * d) * (0.5f * __builtin_amdgcn_rcpf(s * s)) - ls - 0.91893853320467274178f;
   }
   // ---- outputs --------------------------------------------------------------
   const bool keep = alive && live;
