@@ -831,9 +831,12 @@ __global__ __launch_bounds__(PA_THREADS, 512 / PA_THREADS) void policy_act_kerne
   for (int o = 0; o < NOUT; o++) {
     const float d = act[o] - mean[o];
     const float s = std_[o];
-    // log(std) is the log-scale itself wherever exp neither overflowed nor went to 0
-    // (the guarded rows carry std 1: log 0); v_rcp_f32 for 1 / var (1 ulp)
-    const float ls = (s > 0.f && s < INFINITY) ? ((a.forced || ok) ? lsd[o] : 0.f) : logf(s);
+    // log(std) is the log-scale itself (the guarded rows carry std 1: log 0), except
+    // where an f32 exp overflows to inf or rounds to 0 (below ln 2^-150; the hardware
+    // exp may flush the denormals above that, whose log the log-scale stays), as
+    // torch's log(exp(.)) does; v_rcp_f32 for 1 / var (1 ulp)
+    const float l = (a.forced || ok) ? lsd[o] : 0.f;
+    const float ls = (s < INFINITY && l > -103.972f) ? l : logf(s);
     lp[o] = -(d * d) * (0.5f * __builtin_amdgcn_rcpf(s * s)) - ls - 0.91893853320467274178f;
   }
   // ---- outputs --------------------------------------------------------------

@@ -295,6 +295,59 @@ def test_policy_act_direct():
     torch.testing.assert_close(full, torch.where(keep, act, 0.0).double(), rtol=0, atol=0)
 
 
+def test_policy_act_extreme_log_std():
+    """lnw_policy_act with forced actions where the log-std head spans about
+    +-300: scales that overflow to inf and vanish to 0 beside ordinary ones.
+    Log-probabilities against -(x - m)^2 / (2 var) - log(std) - log(sqrt(2 pi))
+    in torch fp32 (torch.distributions' formula; Normal itself refuses such
+    scales), infinities and NaNs in the same places; rows whose log-scale lies
+    within 6 of exp's overflow (88.7), of var's denormal range (-43.7 .. -51.6)
+    or of the scale's rounding to 0 (-103.97) are left out, where the bf16x3 MLP's last-ulp differences may land on either
+    side of the threshold."""
+    import ctypes as C
+    import math
+    from lnw import _abi
+    from lnw.rollout import BatchedActor
+    L = _abi.load()
+    torch.manual_seed(7)
+    a = BatchedActor.for_obs(68).cuda()
+    with torch.no_grad():
+        a.log_std_head.weight.mul_(150.0)
+    E, n = 2000, 4
+    obs = torch.rand((E, n, 68), device="cuda")
+    obs[:, :, :49] = torch.randint(0, 256, (E, n, 49), device="cuda") / 255.0
+    act = torch.rand((E, n, 4), device="cuda")
+    alive = torch.ones((n, E), dtype=torch.uint8, device="cuda")
+    lp = torch.zeros((E, n, 4), device="cuda")
+    ao = torch.zeros((E, n, 4), device="cuda")
+    params = a.packed_policy()
+    pa = _abi.PolicyArgs()
+    pa.obs, pa.E, pa.n, pa.D, pa.own0, pa.A = obs.data_ptr(), E, n, 68, 0, n
+    pa.params, pa.forced, pa.forced_act, pa.fa_env_stride = params.data_ptr(), 1, act.data_ptr(), n * 4
+    pa.alive, pa.act_out, pa.logp_out, pa.act_env_stride = alive.data_ptr(), ao.data_ptr(), lp.data_ptr(), n * 4
+    _abi.check(L.lnw_policy_act(C.byref(pa), None))
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        x = a.features(obs.reshape(E * n, 68))
+        x = torch.tanh(a.fc3(torch.tanh(a.fc2(torch.tanh(a.fc1(x))))))
+        mean, lsd = torch.tanh(a.normal_head(x)), a.log_std_head(x)
+    std = torch.exp(lsd)
+    d = act.reshape(E * n, 4) - mean
+    want = -(d * d) / (2.0 * std * std) - torch.log(std) - 0.5 * math.log(2.0 * math.pi)
+    got = lp.reshape(E * n, 4)
+    edge = ((lsd - 88.7).abs() < 6.0) | ((lsd > -57.6) & (lsd < -37.7)) | ((lsd + 103.97).abs() < 6.0)
+    assert (lsd > 95.0).any() and (lsd < -110.0).any() and ((lsd < -60.0) & (lsd > -98.0)).any()
+    assert (lsd.abs() < 20.0).any()
+    keep = ~edge
+    assert torch.equal(torch.isinf(got[keep]), torch.isinf(want[keep]))
+    assert torch.equal(torch.isnan(got[keep]), torch.isnan(want[keep]))
+    fin = keep & torch.isfinite(want)
+    assert torch.equal(torch.sign(got[keep & torch.isinf(want)]), torch.sign(want[keep & torch.isinf(want)]))
+    # (1 / var is exp(-2 log-scale): the MLP's ~1e-4 absolute error in a log-scale of
+    # -30 is ~2e-4 relative in the quadratic term)
+    torch.testing.assert_close(got[fin], want[fin], rtol=2e-3, atol=2e-3)
+
+
 def _port():
     import socket
     s = socket.socket()
