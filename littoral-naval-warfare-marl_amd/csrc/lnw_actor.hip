@@ -896,16 +896,24 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_arg
 #pragma unroll
     for (int rt = 0; rt < 4; rt++) acc[rt][0] = acc[rt][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
     const f32x4v *F1 = (const f32x4v *)(C + co.w1) + (size_t)w * 2 * dq * WAVE;
-    for (int q = 0; q < dq; q++) {  // (uniform trip count; MFMAs unrolled inside)
+    // (uniform trip count; MFMAs unrolled inside; quad q + 1's rows and weights
+    // are loaded before quad q's MFMAs, so one load latency per wave, not dq)
+    auto load_q = [&](int q, f32x4v (&xb)[4], f32x4v &w0, f32x4v &w1) {
       const int k = 16 * q + 4 * g;
-      f32x4v xb[4];
 #pragma unroll
       for (int rt = 0; rt < 4; rt++) {
         const long long er = e0 + rt * 16 + m;
         xb[rt] = (k < D && er < a.E) ? *(const f32x4v *)(a.obs + er * a.obs_env_stride + (long long)w * D + k)
                                       : f32x4v{0.f, 0.f, 0.f, 0.f};
       }
-      const f32x4v w0 = F1[(0 * dq + q) * WAVE + lane], w1 = F1[(1 * dq + q) * WAVE + lane];
+      w0 = F1[(0 * dq + q) * WAVE + lane];
+      w1 = F1[(1 * dq + q) * WAVE + lane];
+    };
+    f32x4v xb[4], w0, w1;
+    load_q(0, xb, w0, w1);
+    for (int q = 0; q < dq; q++) {
+      f32x4v xn[4], n0, n1;
+      if (q + 1 < dq) load_q(q + 1, xn, n0, n1);
 #pragma unroll
       for (int v = 0; v < 4; v++)
 #pragma unroll
@@ -913,6 +921,12 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(lnw_rollout_post_arg
           acc[rt][0] = mfma4(w0[v], xb[rt][v], acc[rt][0]);
           acc[rt][1] = mfma4(w1[v], xb[rt][v], acc[rt][1]);
         }
+      if (q + 1 < dq) {
+#pragma unroll
+        for (int rt = 0; rt < 4; rt++) xb[rt] = xn[rt];
+        w0 = n0;
+        w1 = n1;
+      }
     }
   #pragma unroll
     for (int rt = 0; rt < 4; rt++)
