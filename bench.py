@@ -93,7 +93,34 @@ def parse():
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary lines (configs 2, 3-shard, 4, 5, melee, march)")
     p.add_argument("--secondary-steps", type=int, default=100)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher plumbing only (runs without a GPU): the ranks start, join the "
+                        "process group and run the barrier / max-over-ranks timing around an "
+                        "empty region; the line's value is null")
     return p.parse_args()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start the N
+    rank processes through torch.distributed.run as a child process, before
+    this process has touched the GPU (nothing here initialises HIP, so no
+    exec-after-GPU-init), with the same arguments. Rank 0 prints the JSON line
+    to the inherited stdout; returns the launcher's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    log(f"bench.py: --gpus {n} without a launcher; starting {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, cwd=ROOT)
 
 
 def log(*a):
@@ -420,12 +447,46 @@ def secondary_lines(args):
     return out
 
 
+def dry_run(args, world, rank):
+    """--dry-run: the launcher and process-group plumbing of an N-rank run
+    without the step (no GPU needed): barrier, an empty timed region, the
+    max-over-ranks reduction, and the line's rank and backend fields."""
+    from lnw import dist
+    dist.barrier()
+    t0 = time.perf_counter()
+    dist.barrier()
+    elapsed = dist.reduce_max([time.perf_counter() - t0])[0]
+    if rank == 0:
+        print(json.dumps({"metric": "env-steps/sec (dry run: launcher plumbing only)", "value": None,
+                          "unit": "env-steps/sec", "n_gpus": world, "steps": 0, "warmup": 0,
+                          "ms_per_step": None, "higher_is_better": True, "dry_run": True,
+                          "barrier_s": elapsed,
+                          "config": {"dist_backend": dist.backend(), "dist_world_size": dist.size(),
+                                     "launcher": os.environ.get("LNW_BENCH_LAUNCHER", "external")}}),
+              flush=True)
+    dist.finalize()
+
+
 def main():
     args = parse()
     global EPISODE_STEPS
     EPISODE_STEPS = args.episode_steps
     from lnw import dist
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's contract names `--gpus N`: without a launcher, become one
+        n_dev = torch.cuda.device_count()  # (does not initialise HIP on this image)
+        if not args.dry_run and "LNW_FORCE_DEVICE" not in os.environ and n_dev < args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but {n_dev} GPU(s) visible")
+            sys.exit(2)
+        os.environ["LNW_BENCH_LAUNCHER"] = "self"
+        sys.exit(launch_ranks(args.gpus))
     world, rank, local = dist.world()
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the rank count must match")
+        sys.exit(2)
+    if args.dry_run:
+        dist.init(os.environ.get("LNW_DIST_BACKEND", "gloo"))
+        return dry_run(args, world, rank)
     # LNW_FORCE_DEVICE / LNW_DIST_BACKEND: the multi-rank test runs two ranks on
     # one GPU over gloo (tests/test_gpu_bench_ranks.py); the driver sets neither
     torch.cuda.set_device(int(os.environ.get("LNW_FORCE_DEVICE", local)))
@@ -488,6 +549,8 @@ def main():
                 "los_mode": args.los_mode,
                 "move_mode": args.move_mode, "parallelism": f"env-shard x{world}",
                 "dist_backend": dist.backend(),
+                "dist_world_size": dist.size(),
+                "launcher": os.environ.get("LNW_BENCH_LAUNCHER", "external" if world > 1 else None),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -561,7 +561,9 @@ __device__ inline bool check_path_dev(const Blocked &blocked, bool start_blocked
 
 // continuous_to_discrete arithmetic (combatant.py:459-471) in the value kind
 // of the action row: float32 rows evaluate in float32 (NEP 50), others in f64.
-// Returns false for non-finite / absurd targets (round(nan) raises).
+// Returns false for a non-finite target (round(nan) raises ValueError and
+// round(inf) OverflowError, combatant.py:470-471); finite targets beyond
+// +-10^6 are only out of the grid.
 __device__ inline bool move_target_dev(int px, int py, int speed, double a2, double a3, int kind,
                                        int &nx, int &ny) {
   double fxd, fyd;
@@ -591,7 +593,7 @@ __device__ inline bool move_target_dev(int px, int py, int speed, double a2, dou
   if (!(fabs(fxd) < 1.0e6) || !(fabs(fyd) < 1.0e6)) {
     nx = -1000000;
     ny = -1000000;
-    return (fxd == fxd) && (fyd == fyd);  // huge but finite: just out of bounds
+    return isfinite(fxd) && isfinite(fyd);  // huge but finite: just out of bounds
   }
   nx = (int)fxd;
   ny = (int)fyd;

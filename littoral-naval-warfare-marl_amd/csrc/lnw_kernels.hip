@@ -2208,7 +2208,10 @@ __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, C
     // split contact step's rows came out with float4s of other rows in about
     // one 45-step 4 096-env run in four ("The split contact step
     // with rows"); 0 in 28 with it, at ~3 us of a 177 us melee step
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef LNW_DIAG
+    if (!(P.dbg_skip & (1 << 25)))  // diagnostics: bit 25 drops the wait (tools/contact_race.py)
+#endif
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_lds_sync();
   }
 }
@@ -3183,6 +3186,8 @@ __device__ __forceinline__ void step_body(
             thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
           else
             thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
+          // round(nan/inf) of engagement * missiles raises (combatant.py:528): flagged, no engagement
+          if (!isfinite(thr_v)) { X.rng.err |= LNW_ERRF_NAN_ROUND; thr_v = 0.0; }
           engage = thr_v > 0.0;
           int tn = (int)COLW(c.tcnt, a);
           if (engage && tn > 0 && !(P.dbg_skip & 65536)) {  // (bit 16: diagnostics, no fire)
@@ -3288,7 +3293,7 @@ __device__ __forceinline__ void step_body(
             const double thr_v = kind_promote(keng, mk) == K_F32
                                      ? (double)rintf((float)engagement * (float)COLB(c.miss_cur, a))
                                      : rint(engagement * (double)COLB(c.miss_cur, a));
-            if (thr_v > 0.0 && COLW(c.tcnt, a) > 0 && !(P.dbg_skip & 65536))
+            if (isfinite(thr_v) && thr_v > 0.0 && COLW(c.tcnt, a) > 0 && !(P.dbg_skip & 65536))
               nd += fire_draws(X, a, engagement, keng);
           }
         }
@@ -3397,6 +3402,8 @@ __device__ __forceinline__ void step_body(
             thr_v = (double)rintf((float)engagement * (float)COLB(c.miss_cur, a));
           else
             thr_v = rint(engagement * (double)COLB(c.miss_cur, a));
+          // round(nan/inf) of engagement * missiles raises (combatant.py:528): flagged, no engagement
+          if (!isfinite(thr_v)) { X.rng.err |= LNW_ERRF_NAN_ROUND; thr_v = 0.0; }
           engage = thr_v > 0.0;
           int tn = (int)COLW(c.tcnt, a);
           if (engage && tn > 0 && !(P.dbg_skip & 65536)) {  // (bit 16: diagnostics, no fire)

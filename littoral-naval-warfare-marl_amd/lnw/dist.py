@@ -40,6 +40,11 @@ def backend():
     return dist.get_backend() if dist.is_initialized() else None
 
 
+def size():
+    """The rank count the process group (RCCL / gloo) reports, or None."""
+    return dist.get_world_size() if dist.is_initialized() else None
+
+
 def _dev():
     return torch.device("cuda", torch.cuda.current_device()) if (
         dist.is_initialized() and dist.get_backend() == "nccl") else torch.device("cpu")

@@ -401,8 +401,13 @@ static int can_move_to(const uint8_t *grid, int G, int thr, int x, int y) {
 }
 
 /* continuous_to_discrete target arithmetic (combatant.py:459-471).
- * kind: K_F32 for np.float32 actions, K_F64/K_PYFLOAT for doubles. */
-void orc_move_target(int px, int py, int speed, double a2, double a3, int kind, int *nx, int *ny) {
+ * kind: K_F32 for np.float32 actions, K_F64/K_PYFLOAT for doubles.
+ * Returns 0 when float_x or float_y is not finite: round() of it raises
+ * (ValueError for nan, OverflowError for inf, combatant.py:470-471); the target
+ * is then (-10^6, -10^6), never feasible. Finite targets beyond +-10^6 are just
+ * out of the grid (Python rounds them to a big int). */
+int orc_move_target(int px, int py, int speed, double a2, double a3, int kind, int *nx, int *ny) {
+    double rx, ry;
     if (kind == K_F32) {
         float course = (float)(2.0 * PY_PI) * (float)a2;
         float dist = (float)speed * (float)a3;
@@ -411,17 +416,24 @@ void orc_move_target(int px, int py, int speed, double a2, double a3, int kind, 
         float dy = (float)sin(deg) * dist;
         float fx = (float)px + dx;
         float fy = (float)py + dy;
-        *nx = (int)nearbyintf(fx);
-        *ny = (int)nearbyintf(fy);
+        rx = (double)nearbyintf(fx);
+        ry = (double)nearbyintf(fy);
     } else {
         double course = 2.0 * PY_PI * a2;
         double dist = (double)speed * a3;
         double deg = py_degrees(course);
         double dx = cos(deg) * dist;
         double dy = sin(deg) * dist;
-        *nx = (int)py_round((double)px + dx);
-        *ny = (int)py_round((double)py + dy);
+        rx = py_round((double)px + dx);
+        ry = py_round((double)py + dy);
     }
+    if (!(fabs(rx) < 1.0e6) || !(fabs(ry) < 1.0e6)) {
+        *nx = *ny = -1000000;
+        return isfinite(rx) && isfinite(ry);
+    }
+    *nx = (int)rx;
+    *ny = (int)ry;
+    return 1;
 }
 
 /* floor division / modulo with Python semantics */
@@ -777,7 +789,8 @@ static void take_action(orc_env *e, int a, const double *act, int kind, double *
     /* new position */
     int feasible = 0, nx = 0, ny = 0;
     if (!e->P.discrete) {
-        orc_move_target(me->x, me->y, ship_speed(me->type), act[2], act[3], kind, &nx, &ny);
+        if (!orc_move_target(me->x, me->y, ship_speed(me->type), act[2], act[3], kind, &nx, &ny))
+            e->err |= ORC_ERR_NAN_ROUND;  /* round(nan/inf), combatant.py:470 */
         if (can_move_to(grid, G, thr, nx, ny) &&
             orc_check_path(grid, G, thr, me->type, me->x, me->y, nx, ny))
             feasible = 1;
@@ -793,6 +806,12 @@ static void take_action(orc_env *e, int a, const double *act, int kind, double *
     int kthr;
     double thr_v = kmul(engagement, keng, me->missiles, me->mkind, &kthr);
     double engagement_threshold = kthr == K_F32 ? (double)nearbyintf((float)thr_v) : nearbyint(thr_v);
+    if (!isfinite(engagement_threshold)) {
+        /* round(nan/inf) of engagement * missiles raises (combatant.py:528): flagged,
+         * and the ship then does not engage */
+        e->err |= ORC_ERR_NAN_ROUND;
+        engagement_threshold = 0.0;
+    }
     int engage = engagement_threshold > 0;
     int destroyed = 0;
     if (engage && me->tl_n > 0) {

@@ -75,6 +75,24 @@ def test_bench_main_two_ranks():
     assert c5["env_steps_per_sec"] == pytest.approx(32768 * 40 / (c5["ms_per_rollout"] / 1e3))
 
 
+def test_bench_gpus_two_self_launched():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts its two
+    ranks itself (torch.distributed.run as a child) and the line reports them."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID", "LNW_BENCH_LAUNCHER")}
+    env.update(LNW_FORCE_DEVICE="0", LNW_DIST_BACKEND="gloo")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+           "--global-envs", "8192", "--no-cpu-baseline", "--no-secondary"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["dist_world_size"] == 2
+    assert line["config"]["launcher"] == "self" and line["config"]["dist_backend"] == "gloo"
+    assert line["config"]["envs_per_gpu"] == 4096 and line["err_envs"] == 0 and line["value"] > 0
+
+
 def test_bench_main_rccl_one_rank():
     """bench.py under torch.distributed.run with one rank: the process group
     is RCCL ("nccl" backend) and the max-over-ranks all_reduce and barriers
@@ -88,5 +106,5 @@ def test_bench_main_rccl_one_rank():
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert line["config"]["dist_backend"] == "nccl"
+    assert line["config"]["dist_backend"] == "nccl" and line["config"]["dist_world_size"] == 1
     assert line["n_gpus"] == 1 and line["err_envs"] == 0 and line["value"] > 0

@@ -47,7 +47,15 @@ def main():
 
     first = None
     good_rows = None
+    dumps = {}
     for r in range(R):
+        # RACE_SKIP_BITS=b: LNW_DEBUG_SKIP for runs >= 1 (diagnostics build via LNW_LIB,
+        # e.g. 33554432 = bit 25: write_obs_t without its per-pass store wait)
+        if os.environ.get("RACE_SKIP_BITS"):
+            if r == 0:
+                os.environ.pop("LNW_DEBUG_SKIP", None)
+            else:
+                os.environ["LNW_DEBUG_SKIP"] = os.environ["RACE_SKIP_BITS"]
         # RACE_REF_NOSPLIT=1: run 0 on the emission path (LNW_NO_SPLIT_ROWS), the reference rows
         if os.environ.get("RACE_REF_NOSPLIT"):
             if r == 0:
@@ -74,6 +82,14 @@ def main():
               flush=True)
         if len(bad) == 0 and good_rows is None:
             good_rows = rows
+        if len(bad) and good_rows is not None and os.environ.get("RACE_DUMP"):
+            # RACE_DUMP=path: the rows of every workgroup with a wrong (step, env), as
+            # written and as they should be (the first clean run), for the offline
+            # source attribution of each wrong float4 (tools/race_chunks.py)
+            keys = sorted({(s_, e // 64) for s_, e in bad.tolist()})[:48]
+            dumps.setdefault("got", []).extend(rows[s_, 64 * w:64 * w + 64] for s_, w in keys)
+            dumps.setdefault("want", []).extend(good_rows[s_, 64 * w:64 * w + 64] for s_, w in keys)
+            dumps.setdefault("key", []).extend((r, s_, w) for s_, w in keys)
         if len(bad) and good_rows is not None:
             for s_, e in bad[:3].tolist():
                 for a in range(8):
@@ -95,6 +111,11 @@ def main():
             first = gh
         else:
             print(f"  vs run 0: {int((gh != first).sum())} (step, env) hashes differ", flush=True)
+    if dumps:
+        np.savez_compressed(os.environ["RACE_DUMP"], got=np.stack(dumps["got"]), want=np.stack(dumps["want"]),
+                            key=np.array(dumps["key"], np.int64))
+        print(f"dumped {len(dumps['key'])} (run, step, workgroup) blocks to {os.environ['RACE_DUMP']}",
+              flush=True)
 
 
 if __name__ == "__main__":
