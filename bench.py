@@ -296,6 +296,30 @@ def ray_march(n=1 << 22, reps=10):
                 rays=n, mean_cells_per_ray=cells / n)
 
 
+def config5_bytes(nb=4, nr=4):
+    """Algorithmic HBM bytes per env-step of config 5's four launches (a 4v4
+    rollout step, blue actor, scripted red; ppo.py:497-605's data flow), each
+    read or written once:
+      observe      state read (26 B/agent + 52 B/env), blue rows out (4 nb + 52
+                   floats each), target-list counts and the RNG counter back;
+      policy       blue rows in, alive / live flags; the f64 action array of the
+                   step (every agent), the rollout's f32 actions and log-probs,
+                   row kinds and the f32 flag out;
+      step         the action array and kinds in, the state read and written back
+                   (contact), f64 rewards, done and cog out;
+      post         blue rows (the critic's input), rewards, done and live in; the
+                   value, rewards, running and live flags out."""
+    A = nb + nr
+    state = A * 26 + 52
+    rows = nb * (4 * nb + 52) * 4
+    out = dict(observe=state + rows + A * 2 + 8,
+               policy=rows + A + 1 + A * 4 * 8 + 2 * nb * 4 * 4 + A + 1,
+               step=A * 4 * 8 + A + 2 * state + A * 8 + 4 + 8,
+               post=rows + nb * 8 + 4 + 1 + 4 + nb * 8 + 1 + 1)
+    out["total"] = sum(out.values())
+    return out
+
+
 def mappo_rollout(total=32768, T=40, reps=3):
     """40-step MAPPO rollouts of `total` envs over the
     ranks (rank r holds lnw.shard.env_range's share, env_id_base = its first
@@ -344,7 +368,16 @@ def mappo_rollout(total=32768, T=40, reps=3):
     torch.cuda.synchronize()
     dtg = timed(r.replay)
     g.close()
-    return dict(env_steps_per_sec=total * T / dtg, ms_per_rollout=dtg * 1e3,
+    # roofline of the whole step (its four launches back to back from the graph):
+    # algorithmic bytes per env-step x this rank's envs / the step's wall time
+    B = config5_bytes()
+    step_s = dtg / T
+    ach = B["total"] * E / step_s / 1e9
+    roof = dict(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=ach / HBM_PEAK_GBS,
+                algorithmic_bytes_per_env_step=B, us_per_step=step_s * 1e6,
+                note="all four launches of a step together (observe, policy, step, post); per-kernel "
+                     "split and PMC traffic in profiles/r06_config5_rocprof.md")
+    return dict(env_steps_per_sec=total * T / dtg, ms_per_rollout=dtg * 1e3, roofline=roof,
                 eager_env_steps_per_sec=total * T / dt, eager_ms_per_rollout=dt * 1e3,
                 envs=total, envs_per_gpu=E, n_gpus=world, steps=T,
                 policy="fused HIP policy step (lnw_policy_act: conv head + MLP + keyed sample + "

@@ -176,9 +176,7 @@ int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8
  * outputs at the output pointers + k * the output strides (elements; a stride
  * 0 makes every step write the same rows, each step's outputs replacing the
  * previous step's as K separate calls would). It makes the K lnw_step
- * launches itself; with LNW_SEQ_FUSED set at lnw_create the templated 4v4
- * default variant runs the K steps in one launch instead (each workgroup moving
- * through them on its own: measured slower, an A/B knob). */
+ * launches itself, back to back on the caller's stream. */
 typedef struct lnw_seq {
   int32_t steps;               /* K >= 1 */
   int64_t act_step, kind_step; /* action elements / row-kind bytes between steps */

@@ -1071,6 +1071,20 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
 #ifdef LNW_PROBE_ONEBLOCK  // probe builds: one block per CU
   if (lds < 84 * 1024) lds = 84 * 1024;
 #endif
+  // One block per CU: head_and_mlp's schedule (every head, a barrier, every MLP)
+  // keeps a head from running beside an MLP only within the block, so no other
+  // block may share the CU. The block asks for more than half of the CU's LDS,
+  // padded up should a future layout (a smaller tile, the weights out of LDS, a
+  // smaller PA_THREADS) need less.
+  static int cu_lds = 0;
+  if (!cu_lds) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || v <= 0)
+      v = 160 * 1024;
+    cu_lds = v;
+  }
+  if (lds <= (size_t)cu_lds / 2) lds = (size_t)cu_lds / 2 + 16;
   if (pa.n_in <= 32)
     policy_act_kernel<32><<<blocks, PA_THREADS, lds, (hipStream_t)stream>>>(pa);
   else

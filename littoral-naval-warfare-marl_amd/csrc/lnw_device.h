@@ -55,13 +55,6 @@ struct KParams {
   int atan_odd;       // the host's bearing table is odd in dy (degrees(atan2(-dy, dx)) == -degrees(atan2(dy, dx))): the group kernel stages its dy >= 0 half
   int no_obs;         // lnw_step without observation outputs (both pointers NULL)
   long long obs_stride[2];  // lnw_observe_ex: floats between envs' rows per side (0: packed)
-  // lnw_step_seq: steps per launch and the element strides between consecutive
-  // steps' action arrays / row kinds / outputs (0: every step uses the same)
-  int seq_steps;
-  long long seq_act, seq_kind, seq_obs[2], seq_rew[2], seq_done, seq_cog;
-  // (lnw_step_seq) the sequence's base pointers: actions, row kinds, obs blue / red,
-  // rewards blue / red, done, cog
-  void *seq_ptr[8];
   int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table, bit13 4-ship phase-S rows stored row by row instead of line-aligned, bit15 the group kernel's fire loop entry by entry
 };
 

@@ -2208,10 +2208,12 @@ __device__ __forceinline__ void write_obs_t(const KParams &P, const KState &S, C
     // split contact step's rows came out with float4s of other rows in about
     // one 45-step 4 096-env run in four ("The split contact step
     // with rows"); 0 in 28 with it, at ~3 us of a 177 us melee step
-#ifdef LNW_DIAG
+#if defined(LNW_DIAG)
     if (!(P.dbg_skip & (1 << 25)))  // diagnostics: bit 25 drops the wait (tools/contact_race.py)
 #endif
+#ifndef LNW_PROBE_NO_OBS_WAIT  // (probe builds: the shipped code without the wait, tools/contact_race.py)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     wave_lds_sync();
   }
 }
@@ -2962,11 +2964,7 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // observation passes go through one workgroup-wide queue that every free wave
 // of a quiet unit serves, so the CU's units finish their stream together
 // instead of 4-5 us apart (the spread of separate workgroups on one CU).
-// SEQ: the body of one step inside lnw_step_seq's loop (step_kernel SEQ, below):
-// a wave that leaves the step early then still meets every barrier its
-// partner wave reaches later in the same step (phase O's), since both go on to
-// the next step instead of exiting.
-template <int NB, int NR, bool CW, bool REFW, int UN, bool PS, bool SEQ>
+template <int NB, int NR, bool CW, bool REFW, int UN, bool PS>
 __device__ __forceinline__ void step_body(
     const KParams &P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
@@ -3110,7 +3108,6 @@ __device__ __forceinline__ void step_body(
       if (emit) emit_wave_t<NB>(P, S, c, duct_col, &prog, obs_b, obs_r, env0);
     }
     prof_stamp(S, 5);
-    if (SEQ && phase_o) __syncthreads();  // wave 0's phase-O barrier
     return;
   }
   if (!qcap && astar && !(P.dbg_skip & 4)) {
@@ -3333,10 +3330,7 @@ __device__ __forceinline__ void step_body(
           for (int a = 0; a < NB; a++) turn(X, a, N, ev, hits, bsx, bsy, nbp, rsx, rsy, nrp, tp, t0);
         }
         __syncthreads();
-        if (wid == 1) {
-          if (SEQ && phase_o) __syncthreads();  // wave 0's phase-O barrier
-          return;
-        }
+        if (wid == 1) return;
         {
           const uint32_t w0 = COLW(cr.pos_cur, 0), w1 = COLW(cr.pos_cur, 1), w2 = COLW(cr.pos_cur, 2),
                          w3 = COLW(cr.pos_cur, 3);
@@ -3487,54 +3481,12 @@ __device__ __forceinline__ void step_body(
   else write_obs(P, S, c, duct_col, obs_b, obs_r, env0, nenv, false);
 }
 
-// One step (SEQ = false: lnw_step), or P.seq_steps steps in one launch
-// (lnw_step_seq): each workgroup steps its own envs through the sequence, step
-// k reading action array k and writing output set k (the P.seq_* strides), so
-// the results are those of seq_steps lnw_step calls. Between steps the
-// workgroup's state stores are drained (vmcnt(0)) before a barrier, and the next
-// step's phase L reads them back through the same CU. No grid-wide barrier: the
-// workgroups drift apart, so one CU's head overlaps another's observation stream
-// and the launch gaps of separate step launches disappear.
-template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false, bool SEQ = false>
+// One step of every env (lnw_step; lnw_step_seq makes one launch per step)
+template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false>
 __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
-  if constexpr (!SEQ) {
-    step_body<NB, NR, CW, REFW, UN, PS, false>(P, S, actions, row_kind, obs_b, obs_r, rew_b, rew_r, done_out,
-                                               cog_out);
-  } else {
-    typedef const __attribute__((address_space(4))) char *KAp;
-    typedef const __attribute__((address_space(4))) KParams *KPp;
-    typedef const __attribute__((address_space(4))) KState *KSp;
-    // the kernarg segment: P at offset 0, S after it at its alignment (the
-    // AMDGPU kernel ABI lays the arguments out in order, each at its alignment)
-    constexpr size_t S_OFF = (sizeof(KParams) + alignof(KState) - 1) / alignof(KState) * alignof(KState);
-    for (int k = 0;; k++) {
-      // the kernel arguments read afresh every step (through an opaque copy of
-      // the kernarg segment pointer; not &P, which would make the compiler copy
-      // the arguments to scratch), the sequence's pointers among them (seq_ptr):
-      // otherwise everything the step derives from them is hoisted out of the
-      // loop and held live across it, and the body spills
-      KAp ka = (KAp)__builtin_amdgcn_kernarg_segment_ptr();
-      asm volatile("" : "+s"(ka));
-      KPp pp = (KPp)ka;
-      KSp sp = (KSp)(ka + S_OFF);
-      const KParams &Pk = *(const KParams *)pp;
-      if (k >= Pk.seq_steps) break;
-      const long long asz = Pk.act_dtype == LNW_ACT_F64 ? 8 : 4, rsz = Pk.rew_f64 ? 8 : 4;
-      auto adv = [&](int j, long long stride, long long sz) {
-        char *p = (char *)Pk.seq_ptr[j];
-        return p ? (void *)(p + (long long)k * stride * sz) : nullptr;
-      };
-      step_body<NB, NR, CW, REFW, UN, PS, true>(
-          Pk, *(const KState *)sp, adv(0, Pk.seq_act, asz), (const uint8_t *)adv(1, Pk.seq_kind, 1),
-          (float *)adv(2, Pk.seq_obs[0], 4), (float *)adv(3, Pk.seq_obs[1], 4),
-          (float *)adv(4, Pk.seq_rew[0], rsz), (float *)adv(5, Pk.seq_rew[1], rsz),
-          (int32_t *)adv(6, Pk.seq_done, 4), (float *)adv(7, Pk.seq_cog, rsz));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's state stores done
-      __syncthreads();
-    }
-  }
+  step_body<NB, NR, CW, REFW, UN, PS>(P, S, actions, row_kind, obs_b, obs_r, rew_b, rew_r, done_out, cog_out);
 }
 
 #include "lnw_group.inc"
@@ -3967,7 +3919,6 @@ struct lnw_handle {
   bool no_split_rows = false;  // LNW_NO_SPLIT_ROWS (A/B): row-writing contact steps keep phase S on one wave
   bool store_wt = false;
   bool units_fit = false;  // UNITS blocks of the step layout fit one workgroup (lnw_load_terrain)
-  bool seq_fused = false;  // LNW_SEQ_FUSED: lnw_step_seq's one-launch sequence kernels
   bool contact = false;  // lnw_set_variant: contact-heavy phase-S code in the templated kernels
   int last_kernel = LNW_KERNEL_NONE;     // lnw_step_kernel: what the last lnw_step launched
   bool has_medium = false;               // the spawn spec has medium ships (runtime-size kernels only)
@@ -4313,9 +4264,6 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->no_split_rows = getenv("LNW_NO_SPLIT_ROWS") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
-  // LNW_SEQ_FUSED (A/B): lnw_step_seq through the sequence kernels (one launch
-  // for the K steps) instead of K lnw_step launches; measured slower
-  h->seq_fused = getenv("LNW_SEQ_FUSED") != nullptr;
   h->kp.xcd_remap = getenv("LNW_NO_XCD_REMAP") == nullptr ? 1 : 0;
   // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
   // terrain mask instead of loading LOS-table words (A/B)
@@ -4601,11 +4549,8 @@ int lnw_reset(lnw_handle *h, const uint8_t *env_mask_dev, const lnw_spawn *spawn
 }
 
 namespace {
-constexpr int STEP_NOT_FUSED = 1;  // step_launch: this shape has no fused sequence kernel
-// lnw_step's launch; with seq (lnw_step_seq) the fused sequence kernel when the
-// shape has one (units kernel, templated 4v4 default variant), else
-// STEP_NOT_FUSED before anything is launched
-int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t action_dtype,
+// lnw_step's launch (lnw_step_seq makes one per step)
+int step_launch(lnw_handle *h, void *actions_dev, int32_t action_dtype,
                 const uint8_t *row_kind_dev, float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev,
                 float *rew_red_dev, int32_t *done_dev, float *cog_dev, void *stream) {
   if (!h || !actions_dev) return fail(LNW_EINVAL, "null argument");
@@ -4623,21 +4568,6 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
   k.no_obs = obs_blue_dev == nullptr ? 1 : 0;
   k.dbg_skip = h->dbg_skip;
   k.store_wt = h->store_wt;
-  k.seq_steps = 1;
-  if (seq) {
-    k.seq_steps = seq->steps;
-    k.seq_act = seq->act_step;
-    k.seq_kind = seq->kind_step;
-    k.seq_obs[0] = seq->obs_blue_step;
-    k.seq_obs[1] = seq->obs_red_step;
-    k.seq_rew[0] = seq->rew_blue_step;
-    k.seq_rew[1] = seq->rew_red_step;
-    k.seq_done = seq->done_step;
-    k.seq_cog = seq->cog_step;
-    void *const ptrs[8] = {actions_dev, (void *)row_kind_dev, obs_blue_dev, obs_red_dev,
-                           rew_blue_dev, rew_red_dev, done_dev, cog_dev};
-    for (int j = 0; j < 8; j++) k.seq_ptr[j] = ptrs[j];
-  }
   KState s = make_state(h);
   size_t lds = step_launch_lds_bytes(h, k.epw);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
@@ -4651,9 +4581,6 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
   // the units kernel (LNW_NO_UNITS keeps one unit per workgroup)
   const bool units = templated && h->nb == 4 && !h->contact && !h->no_units && h->units_fit && k.epw == EPW &&
                      k.los_mode == 0 && h->E % (EPW * UNITS) == 0 && !(h->dbg_skip & (1 | 2 | 512));
-  // lnw_step_seq's fused kernels: the units kernel and the templated 4v4 default variant
-  const bool seq_fused = units || (templated && h->nb == 4 && !h->contact && k.los_mode != 2);
-  if (seq && (!seq_fused || h->prof || !h->seq_fused)) return STEP_NOT_FUSED;
   // per-unit records (LNW_PROF) of the kernel launched below (the group kernel has its own grid)
   const unsigned nwg = use_group ? (unsigned)((h->E + GEPW - 1) / GEPW) : grid.x;
   if (h->prof) {
@@ -4676,16 +4603,7 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
                    : k.los_mode == 2 ? LNW_KERNEL_REFLOS
                    : templated ? (cw ? LNW_KERNEL_TEAM_CONTACT : LNW_KERNEL_TEAM)
                    : use_group ? LNW_KERNEL_GROUP : LNW_KERNEL_GENERIC;
-  if (units && seq) {
-    step_kernel<4, 4, false, false, UNITS, false, true><<<dim3(h->E / (EPW * UNITS)), dim3(2 * WAVE * UNITS),
-                                                          (size_t)UNITS * ((lds + 15) & ~(size_t)15), st>>>(
-        k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev,
-        cog_dev);
-  } else if (seq) {
-    step_kernel<4, 4, false, false, 1, false, true><<<grid, dim3(2 * WAVE), lds, st>>>(
-        k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev,
-        cog_dev);
-  } else if (units) {
+  if (units) {
     // 4 units of 64 envs per workgroup, one workgroup per CU (step_kernel UN)
     step_kernel<4, 4, false, false, UNITS><<<dim3(h->E / (EPW * UNITS)), dim3(2 * WAVE * UNITS),
                                              (size_t)UNITS * ((lds + 15) & ~(size_t)15), st>>>(
@@ -4727,7 +4645,7 @@ int step_launch(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t ac
 int lnw_step(lnw_handle *h, void *actions_dev, int32_t action_dtype, const uint8_t *row_kind_dev,
              float *obs_blue_dev, float *obs_red_dev, float *rew_blue_dev, float *rew_red_dev,
              int32_t *done_dev, float *cog_dev, void *stream) {
-  return step_launch(h, nullptr, actions_dev, action_dtype, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev,
+  return step_launch(h, actions_dev, action_dtype, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev,
                      rew_red_dev, done_dev, cog_dev, stream);
 }
 
@@ -4739,16 +4657,15 @@ int lnw_step_seq(lnw_handle *h, const lnw_seq *seq, void *actions_dev, int32_t a
   if (seq->act_step < 0 || seq->kind_step < 0 || seq->obs_blue_step < 0 || seq->obs_red_step < 0 ||
       seq->rew_blue_step < 0 || seq->rew_red_step < 0 || seq->done_step < 0 || seq->cog_step < 0)
     return fail(LNW_EINVAL, "negative step stride");
-  const int rc = step_launch(h, seq, actions_dev, action_dtype, row_kind_dev, obs_blue_dev, obs_red_dev,
-                             rew_blue_dev, rew_red_dev, done_dev, cog_dev, stream);
-  if (rc != STEP_NOT_FUSED) return rc;
-  // no fused kernel for this shape: K launches
+  // K launches back to back on the caller's stream. (Round 5 measured one launch
+  // in which each workgroup ran its envs through the K steps: parity with K
+  // launches at best, DESIGN.md "Action sequences in one call"; removed.)
   const long long asz = action_dtype == LNW_ACT_F64 ? 8 : 4, rsz = h->kp.rew_f64 ? 8 : 4;
   for (int k = 0; k < seq->steps; k++) {
     auto adv = [&](const void *p, long long stride, long long sz) {
       return p ? (void *)((char *)p + (long long)k * stride * sz) : nullptr;
     };
-    if (int e = step_launch(h, nullptr, adv(actions_dev, seq->act_step, asz), action_dtype,
+    if (int e = step_launch(h, adv(actions_dev, seq->act_step, asz), action_dtype,
                             (const uint8_t *)adv(row_kind_dev, seq->kind_step, 1),
                             (float *)adv(obs_blue_dev, seq->obs_blue_step, 4),
                             (float *)adv(obs_red_dev, seq->obs_red_step, 4),

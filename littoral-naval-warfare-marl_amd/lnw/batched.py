@@ -228,8 +228,10 @@ class BatchedGame:
         if keep == "last":
             out = self._outd
         elif keep == "all":
-            out = {k: torch.zeros((K,) + tuple(v.shape), dtype=v.dtype, device=self.device)
-                   for k, v in self._outd.items()}
+            # uninitialised: every step writes every element of its output set (a
+            # sunk ship's row as zeros); no observation tensors when obs=False
+            out = {k: torch.empty((K,) + tuple(v.shape), dtype=v.dtype, device=self.device)
+                   for k, v in self._outd.items() if obs or not k.startswith("obs_")}
             sq.obs_blue_step, sq.obs_red_step = self.E * self.nb * self.Db, self.E * self.nr * self.Dr
             sq.rew_blue_step, sq.rew_red_step = self.E * self.nb, self.E * self.nr
             sq.done_step = sq.cog_step = self.E
@@ -237,6 +239,8 @@ class BatchedGame:
             raise ValueError("keep must be 'last' or 'all'")
         p = {k: _ptr(v) for k, v in out.items()}
         ob, orr = (p["obs_blue"], p["obs_red"]) if obs else (None, None)
+        if not obs:
+            sq.obs_blue_step = sq.obs_red_step = 0
         check(self.L.lnw_step_seq(self.h, C.byref(sq), a.data_ptr(), dt, rk, ob, orr, p["rew_blue"],
                                   p["rew_red"], p["done"], p["cog"],
                                   torch.cuda.current_stream(self.device).cuda_stream))

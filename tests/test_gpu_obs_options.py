@@ -141,9 +141,11 @@ def test_policy_act_strided_input_equals_packed(with_live):
     step t (obs_in_env_stride) gives the outputs of the packed [E][n][D] rows
     bit for bit, call after call, and in place (obs_out == obs) leaves live
     envs' rows alone and zeroes the ended ones. E = 32 768 (config 5's size):
-    two blocks per CU, the shape at which the round-4 kernel's spilled
-    registers came back wrong in lanes 48-63 of the second block's waves
-    (DESIGN.md, "The policy reading its rows in place")."""
+    512-thread blocks, one per CU, two waves per SIMD — the shape at which a
+    wave's head running beside its SIMD partner's MLP came back wrong in lanes
+    48-63 (DESIGN.md, "The policy kernel's nondeterminism"), which
+    head_and_mlp's schedule (every head, a barrier, every MLP) and the host's
+    one-block-per-CU LDS request rule out; 12 calls compared bit for bit."""
     import ctypes as C
     from lnw import _abi
     from lnw.rollout import BatchedActor
@@ -162,7 +164,7 @@ def test_policy_act_strided_input_equals_packed(with_live):
     params = a.packed_policy()
     call = torch.zeros(1, dtype=torch.int64, device="cuda")
     res = []
-    for rep, strided in enumerate([False] + [True] * 6):
+    for rep, strided in enumerate([False] + [True] * 11):
         lp = torch.zeros((E, n, 4), device="cuda")
         ac = torch.zeros((E, n, 4), device="cuda")
         full = torch.zeros((E, 2 * n, 4), dtype=torch.float64, device="cuda")

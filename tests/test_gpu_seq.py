@@ -1,8 +1,6 @@
 """lnw_step_seq (BatchedGame.step_seq): K steps of an action sequence known
-ahead of time in one call. Its results must be those of K lnw_step calls — the
-K launches it makes by default and, under LNW_SEQ_FUSED, the one-launch
-sequence kernels (the units kernel and the templated 4v4 default variant, where
-each workgroup moves through the K steps on its own) alike: every step's observations, rewards, done
+ahead of time in one call (K launches on the caller's stream). Its results
+must be those of K lnw_step calls: every step's observations, rewards, done
 and cog, the action rows as each step left them (an untrained red's salvo
 write-back, game.py:375-379) and the whole state afterwards, bit for bit. The
 workloads cross the 40-step horizon's in-kernel auto-reset and mix quiet and
@@ -34,8 +32,8 @@ CASES = {
     "shard8192": dict(E=8192, epw=0, block=16, nb=4, trained_red=True, kernel="team"),
     # a partial last workgroup and 32 envs per workgroup
     "partial": dict(E=1000, epw=32, block=32, nb=4, trained_red=False, kernel="team"),
-    # no fused kernel: 3v3 runs K lnw_step launches
-    "fallback3v3": dict(E=640, epw=0, block=64, nb=3, trained_red=True, kernel="team"),
+    # the 3v3 templated kernel
+    "team3v3": dict(E=640, epw=0, block=64, nb=3, trained_red=True, kernel="team"),
 }
 
 
@@ -65,14 +63,9 @@ def _same(x, y):
     return torch.equal(x, y)
 
 
-@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_step_seq_equals_steps(name, fused, monkeypatch):
+def test_step_seq_equals_steps(name):
     from lnw import _abi
-    if fused:  # the one-launch sequence kernels (LNW_SEQ_FUSED, read at lnw_create)
-        monkeypatch.setenv("LNW_SEQ_FUSED", "1")
-    else:
-        monkeypatch.delenv("LNW_SEQ_FUSED", raising=False)
     cs = CASES[name]
     grid = _oracle.load_fixture("grids.npz")["grid100"]
     E, nb, K = cs["E"], cs["nb"], 45
@@ -111,14 +104,13 @@ def test_step_seq_equals_steps(name, fused, monkeypatch):
         g.close()
 
 
-def test_step_seq_vs_oracle_shard(monkeypatch):
-    """The fused sequence at config 3's per-GPU shard (8 192 envs, quiet direct
-    mode, mixed quiet / fighting workgroups) against the CPU oracle directly:
-    45 steps in one launch, per (step, env) observation hashes, done, rewards
-    and cog (orc_fullsize_range)."""
+def test_step_seq_vs_oracle_shard():
+    """A sequence at config 3's per-GPU shard (8 192 envs, quiet direct mode,
+    mixed quiet / fighting workgroups) against the CPU oracle directly: 45
+    steps in one call, per (step, env) observation hashes, done, rewards and
+    cog (orc_fullsize_range)."""
     from lnw.batched import BatchedGame
     from lnw.config import Scenario
-    monkeypatch.setenv("LNW_SEQ_FUSED", "1")
     grid = _oracle.load_fixture("grids.npz")["grid100"]
     E, S, seed = 8192, 45, 313
     pos = np.array([REF_SPAWNS] * E, np.int32)
@@ -145,3 +137,28 @@ def test_step_seq_vs_oracle_shard(monkeypatch):
     assert np.allclose(gr, orw, rtol=0, atol=1e-5)
     assert np.allclose(gc, oc, rtol=0, atol=1e-5, equal_nan=True)
     assert (gd == 0).any()
+
+
+def test_step_seq_obs_false_keep_all():
+    """keep="all" with obs=False: no observation tensors are allocated, and the
+    other outputs equal K step(obs=False) calls."""
+    from lnw.batched import BatchedGame
+    from lnw.config import Scenario
+    grid = _oracle.load_fixture("grids.npz")["grid100"]
+    E, K = 256, 6
+    acts = torch.from_numpy(np.random.default_rng(3).random((K, E, 8, 4), dtype=np.float32)).cuda()
+    outs = []
+    for mode in ("steps", "seq"):
+        g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=Scenario(landing_ops=False), grid=grid, seed=9)
+        g.reset(positions=REF_SPAWNS, pos_per_env=torch.from_numpy(_melee(grid, E, seed=4)))
+        if mode == "steps":
+            outs.append([{k: v.clone() for k, v in g.step(acts[k].clone(), obs=False).items()
+                          if not k.startswith("obs_")} for k in range(K)])
+        else:
+            got = g.step_seq(acts.clone(), obs=False, keep="all")
+            assert not any(k.startswith("obs_") for k in got)
+            outs.append([{n: v[k] for n, v in got.items()} for k in range(K)])
+        g.close()
+    for a, b in zip(*outs):
+        for n in a:
+            assert _same(a[n], b[n]), n

@@ -1,4 +1,4 @@
-// Probe (round 5, DESIGN.md "The policy reading its rows in place"): can a VALU
+// Probe (round 5, DESIGN.md "The policy kernel's nondeterminism"): can a VALU
 // write to the data or address VGPR of a ds_write_b128, issued right after it,
 // change what the LDS write stores when the LDS is busy with other waves?
 // lnw_policy_act wrote its fc1 tile with eight ds_write_b128 and hipcc let the

@@ -71,10 +71,88 @@ def trace_only(tag, cmd, steps):
     print("\n".join(lines))
 
 
+C5_FAMILIES = (("observe", "observe_kernel"), ("policy", "policy_act_kernel"), ("step", "step_kernel"),
+                ("post", "rollout_post_kernel"))
+
+
+def family_counters(d, stem):
+    """Per-launch mean of every counter of a --pmc pass, per config-5 kernel family."""
+    path = os.path.join(OUT, d, f"{stem}_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}
+    acc = defaultdict(float)
+    disp = defaultdict(set)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            fam = next((k for k, sub in C5_FAMILIES if sub in r["Kernel_Name"]), None)
+            if fam is None:
+                continue
+            acc[(fam, r["Counter_Name"])] += float(r["Counter_Value"])
+            disp[(fam, r["Counter_Name"])].add(r["Dispatch_Id"])
+    out = defaultdict(dict)
+    for (fam, name), v in acc.items():
+        out[fam][name] = v / len(disp[(fam, name)])
+    return out
+
+
+def config5(tag, cmd, envs):
+    """profiles/<tag>_rocprof.md for config 5: each of the four launches of a
+    rollout step with its mean time, algorithmic bytes (bench.config5_bytes),
+    PMC traffic 2 x FETCH_SIZE + WRITE_SIZE and SQ counters."""
+    import bench
+    d = os.path.join(OUT, tag)
+    stats = os.path.join(d, "kt", "kt_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    avg = {}
+    for fam, sub in C5_FAMILIES:
+        for r in rows:
+            if sub in r["Name"] and fam not in avg:
+                avg[fam] = (float(r["AverageNs"]) / 1e3, short(r["Name"]), int(r["Calls"]))
+    pmc = defaultdict(dict)
+    for sub in ("fetch", "write", "sq", "sq2"):
+        for fam, cs in family_counters(os.path.join(tag, sub), sub).items():
+            pmc[fam].update(cs)
+    B = bench.config5_bytes()
+    lines = [f"# rocprofv3, config 5: {cmd}", "",
+             f"{envs} envs (4v4, blue actor, scripted red) per launch; algorithmic bytes per env-step from "
+             "bench.config5_bytes; PMC per launch (mean), separate --pmc passes; traffic = 2 x FETCH_SIZE + "
+             "WRITE_SIZE (gfx950 correction).", "",
+             "| launch | kernel | calls | avg us | alg B/env-step | alg MB | frac of 8 TB/s | PMC MB | PMC/alg "
+             "| WAIT_ANY/WAVE_CYC | VALU/WAVE_CYC |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
+    tot_t = tot_b = 0.0
+    for fam, _ in C5_FAMILIES:
+        if fam not in avg:
+            continue
+        t, name, calls = avg[fam]
+        alg = B[fam] * envs
+        tot_t += t
+        tot_b += alg
+        p = pmc.get(fam, {})
+        traf = (2 * p["FETCH_SIZE"] + p["WRITE_SIZE"]) * 1024 if "FETCH_SIZE" in p and "WRITE_SIZE" in p else None
+        wc = p.get("SQ_WAVE_CYCLES")
+        wait = f"{p['SQ_WAIT_ANY'] / wc:.2f}" if wc and "SQ_WAIT_ANY" in p else "-"
+        valu = f"{p['SQ_ACTIVE_INST_VALU'] / wc:.2f}" if wc and "SQ_ACTIVE_INST_VALU" in p else "-"
+        lines.append(f"| {fam} | {name[:48]} | {calls} | {t:.1f} | {B[fam]} | {alg / 1e6:.1f} | "
+                     f"{alg / (t * 1e-6) / 8e12:.3f} | {'-' if traf is None else f'{traf / 1e6:.1f}'} | "
+                     f"{'-' if traf is None else f'{traf / alg:.2f}'} | {wait} | {valu} |")
+    lines += ["", f"Step (four launches): {tot_t:.1f} us of kernel time, {tot_b / 1e6:.1f} MB algorithmic -> "
+                  f"{tot_b / (tot_t * 1e-6) / 8e12:.3f} of 8 TB/s", "", "Raw counters per launch:"]
+    for fam, _ in C5_FAMILIES:
+        for k in sorted(pmc.get(fam, {})):
+            lines.append(f"- {fam} {k}: {pmc[fam][k]:,.0f}")
+    open(os.path.join(PROF, f"{tag}_rocprof.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
 def main():
     import hashlib
     import bench
     tag = sys.argv[1]
+    if "--config5" in sys.argv:
+        return config5(tag, sys.argv[sys.argv.index("--cmd") + 1] if "--cmd" in sys.argv else "",
+                       int(sys.argv[sys.argv.index("--envs") + 1]) if "--envs" in sys.argv else 32768)
     key = sys.argv[sys.argv.index("--key") + 1] if "--key" in sys.argv else None
     if key is None:  # kernel trace only (config 5): the stats table and the per-step split
         return trace_only(tag, sys.argv[sys.argv.index("--cmd") + 1] if "--cmd" in sys.argv else "",

@@ -1,4 +1,4 @@
-// Probe (round 5, DESIGN.md "The policy reading its rows in place"): does a
+// Probe (round 5, DESIGN.md "The policy kernel's nondeterminism"): does a
 // VALU write to a VMEM store's data register, issued right after the store,
 // change what the store writes? The round-4 policy kernel spilled a register
 // with scratch_store_dwordx2 and overwrote it with the next instruction; its
