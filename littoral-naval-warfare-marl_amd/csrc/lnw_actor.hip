@@ -356,7 +356,7 @@ __device__ __forceinline__ f32x4v mfma32(const bf16x8 &a, const bf16x8 &b, f32x4
 // acc[rt][nt] += W (planes F: hi | mid | lo, each bf16x8 [nt][p][lane]) x X
 template <int NTO, int Q>
 __device__ __forceinline__ void mfma_layer3(const bf16x8 *__restrict__ F, const f32x4v (&xb)[4][Q],
-                                            f32x4v (&acc)[4][NTO], int lane) {
+                                            f32x4v (&acc)[4][NTO], int lane, bf16x8 *split_save = nullptr) {
   static_assert(Q % 2 == 0, "k in pairs of quads");
   constexpr int QP = Q / 2, PL = NTO * QP * WAVE;  // plane stride (bf16x8)
 #pragma unroll
@@ -364,6 +364,14 @@ __device__ __forceinline__ void mfma_layer3(const bf16x8 *__restrict__ F, const 
     bf16x8 b0[4], b1[4], b2[4];
 #pragma unroll
     for (int rt = 0; rt < 4; rt++) split3(xb[rt][2 * p], xb[rt][2 * p + 1], b0[rt], b1[rt], b2[rt]);
+    if (split_save && p == 0) {  // (diagnostics probe 16)
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) {
+        split_save[3 * rt] = b0[rt];
+        split_save[3 * rt + 1] = b1[rt];
+        split_save[3 * rt + 2] = b2[rt];
+      }
+    }
 #pragma unroll
     for (int nt = 0; nt < NTO; nt++) {
       const int i = (nt * QP + p) * WAVE + lane;
@@ -422,9 +430,13 @@ __host__ __device__ constexpr int mlp_bf16x8() {
 
 // fc1 / fc2 / fc3 and both heads of the wave's 64 rows on the matrix cores
 // (xb: fc1's B operand), then each row's head outputs brought to its own lane
+// (hh_save, xb_save: diagnostics probe 14 only)
 template <int Q1>
 __device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const bf16x8 *Fw, const float *xt, int lane,
-                                          int g, int m, float (&mean)[NOUT], float (&lsd)[NOUT]) {
+                                          int g, int m, float (&mean)[NOUT], float (&lsd)[NOUT],
+                                          f32x4v *hh_save = nullptr, f32x4v *xb_save = nullptr,
+                                          f32x4v *layers_save = nullptr, bf16x8 *split_save = nullptr,
+                                          f32x4v *pre_save = nullptr) {
   constexpr int KS = 16 * Q1 + 4;  // the tile's row stride (policy_act_kernel)
   const lnw_policy_args &a = pa.a;
   f32x4v xb[4][Q1];
@@ -432,26 +444,60 @@ __device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const bf16x8 *Fw
   for (int rt = 0; rt < 4; rt++)
 #pragma unroll
     for (int q = 0; q < Q1; q++) xb[rt][q] = *(const f32x4v *)(xt + (rt * 16 + m) * KS + 16 * q + 4 * g);
+  if (xb_save) {
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int q = 0; q < Q1; q++) xb_save[rt * Q1 + q] = xb[rt][q];
+  }
   // weights: three bf16 planes per layer (mfma_layer3), layers in order
   // Fw: the three bf16 planes of every layer (global, or the block's LDS copy)
   constexpr int O2 = 3 * 4 * (Q1 / 2) * WAVE, O3 = O2 + 3 * 4 * 2 * WAVE, OH = O3 + 3 * 2 * 2 * WAVE;
   const float *bias = a.params + pa.off_b1;  // b1 [64] | b2 [64] | b3 [32]
   f32x4v h1[4][4];
   bias_init<4>(bias, h1, g);
-  mfma_layer3<4, Q1>(Fw, xb, h1, lane);
+  mfma_layer3<4, Q1>(Fw, xb, h1, lane, split_save);
+  if (pre_save) {  // (diagnostics probe 16: fc1 before the activation)
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int nt = 0; nt < 4; nt++) pre_save[rt * 4 + nt] = h1[rt][nt];
+  }
   tanh_all<4>(h1);
+  if (layers_save) {  // probe 15: [layer 0..2][rt][nt] (h1, h2: 4 nt; h3: 2)
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int nt = 0; nt < 4; nt++) layers_save[(0 * 4 + rt) * 4 + nt] = h1[rt][nt];
+  }
   f32x4v h2[4][4];
   bias_init<4>(bias + 64, h2, g);
   mfma_layer3<4, 4>(Fw + O2, h1, h2, lane);
   tanh_all<4>(h2);
+  if (layers_save) {
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int nt = 0; nt < 4; nt++) layers_save[(1 * 4 + rt) * 4 + nt] = h2[rt][nt];
+  }
   f32x4v h3[4][2];
   bias_init<2>(bias + 128, h3, g);
   mfma_layer3<2, 4>(Fw + O3, h2, h3, lane);
   tanh_all<2>(h3);
+  if (layers_save) {
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++) layers_save[(2 * 4 + rt) * 4 + nt] = h3[rt][nt];
+  }
   f32x4v hh[4][1];
 #pragma unroll
   for (int rt = 0; rt < 4; rt++) hh[rt][0] = f32x4v{0.f, 0.f, 0.f, 0.f};
   mfma_layer3<1, 2>(Fw + OH, h3, hh, lane);
+  if (hh_save) {
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) hh_save[rt] = hh[rt][0];
+  }
   // head outputs of row 16 rt + m sit in lane m (normal head, n = v) and lane
   // 16 + m (log-std head, n = 4 + v) of tile rt: bring row `lane` to lane
   // `lane` (rt = g) for the per-row sampling below
@@ -473,7 +519,7 @@ __device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const bf16x8 *Fw
 // A wave's rows up to the fc1 tile: conv head + LayerNorm (one row per lane),
 // the observation copy for the rollout buffer, and the LayerNorm outputs into
 // the wave's fc1 input tile in LDS (xt) for mlp_heads.
-#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12
+#if defined(LNW_PROBE_DISTURB) && (LNW_PROBE_DISTURB >= 12)
 // Diagnostics probe 12: the first head of every wave (all heads at once) saves
 // each stage of its rows here; the partner's second head, run while the other
 // wave of its SIMD runs its MLP, compares stage by stage (window loads, pooled
@@ -481,7 +527,15 @@ __device__ __forceinline__ void mlp_heads(const PolicyArgs &pa, const bf16x8 *Fw
 // outputs) and counts rows that differ per stage and lane (lnw_probe_counts).
 constexpr int PROBE_ROWS = 131072, PROBE_W = 256;
 __device__ float probe_buf[(size_t)PROBE_ROWS * PROBE_W];
-__device__ unsigned probe_cnt[5 * 64];
+constexpr int PROBE_STAGES = 10;
+#if LNW_PROBE_DISTURB >= 15
+__device__ f32x4v probe_layers[(size_t)131072 * 48];  // probe 15: every lane's h1 / h2 / h3 from its phase run
+#endif
+#if LNW_PROBE_DISTURB == 16
+__device__ bf16x8 probe_split[(size_t)131072 * 12];  // probe 16: fc1's bf16 split terms (k-pair 0), per rt
+__device__ f32x4v probe_pre[(size_t)131072 * 16];    // probe 16: fc1 before tanh
+#endif
+__device__ unsigned probe_cnt[PROBE_STAGES * 64];
 template <int N>
 __device__ __forceinline__ void probe_stage(int cmp, int stage, long long row, int off, const float (&v)[N],
                                             int lane) {
@@ -497,7 +551,11 @@ __device__ __forceinline__ void probe_stage(int cmp, int stage, long long row, i
   for (int k = 0; k < N; k++) bad = bad || __float_as_uint(b[k]) != __float_as_uint(v[k]);
   if (bad) atomicAdd(&probe_cnt[stage * 64 + lane], 1u);
 }
+#if LNW_PROBE_DISTURB == 12
 #define PROBE_STAGE(st, off, v) probe_stage(probe_cmp, st, r0 + (threadIdx.x & ~(WAVE - 1)) + lane, off, v, lane)
+#else
+#define PROBE_STAGE(st, off, v) ((void)0)
+#endif
 #else
 #define PROBE_STAGE(st, off, v) ((void)0)
 #endif
@@ -581,6 +639,32 @@ __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *
   for (int k4 = 0; k4 < NI / 4; k4++)
     *(f32x4v *)(xt + lane * KS + 4 * k4) = f32x4v{u[4 * k4], u[4 * k4 + 1], u[4 * k4 + 2], u[4 * k4 + 3]};
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB >= 13
+  // Diagnostics probe 13 (the head/MLP overlap schedule of probe 10): every head
+  // saves the row it wrote; the second head (probe_cmp, beside the SIMD
+  // partner's MLP) reads its tile row back at once and counts lanes whose
+  // bytes differ from what it wrote (stage 0); head_and_mlp checks the tile
+  // again just before this wave's own MLP (stage 1)
+  {
+    const long long grow = r0 + (threadIdx.x & ~(WAVE - 1)) + lane;
+    if (grow < PROBE_ROWS) {
+      float *b = probe_buf + (size_t)grow * PROBE_W;
+#pragma unroll
+      for (int k = 0; k < NI; k++) b[k] = u[k];
+    }
+    if (probe_cmp) {
+      bool bad = false;
+#pragma unroll
+      for (int k4 = 0; k4 < NI / 4; k4++) {
+        f32x4v v = *(const f32x4v *)(xt + lane * KS + 4 * k4);
+        asm volatile("" : "+v"(v));
+#pragma unroll
+        for (int j = 0; j < 4; j++) bad = bad || __float_as_uint(v[j]) != __float_as_uint(u[4 * k4 + j]);
+      }
+      if (bad) atomicAdd(&probe_cnt[0 * 64 + lane], 1u);
+    }
+  }
+#endif
 }
 
 #ifdef LNW_PROBE_DISTURB
@@ -698,10 +782,64 @@ __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *
     nph = r2 + 1 > nph ? r2 + 1 : nph;
     rank = w2 == wv ? r2 : rank;
   }
+#if LNW_PROBE_DISTURB >= 14
+  f32x4v hh1[4];
+#endif
   for (int ph = 0; ph < nph; ph++) {
+#if LNW_PROBE_DISTURB == 13 || LNW_PROBE_DISTURB == 14  // this wave's tile row against what its head wrote, just before its MLP
+    if (ph == rank) {
+      constexpr int KS = NI + 4;
+      const long long grow = r0 + (threadIdx.x & ~(WAVE - 1)) + lane;
+      bool bad = false;
+      if (grow < PROBE_ROWS) {
+        const float *b = probe_buf + (size_t)grow * PROBE_W;
+#pragma unroll
+        for (int k4 = 0; k4 < NI / 4; k4++) {
+          f32x4v v = *(const f32x4v *)(warea + lane * KS + 4 * k4);
+          asm volatile("" : "+v"(v));
+#pragma unroll
+          for (int j = 0; j < 4; j++) bad = bad || __float_as_uint(v[j]) != __float_as_uint(b[4 * k4 + j]);
+        }
+      }
+      if (bad) atomicAdd(&probe_cnt[1 * 64 + lane], 1u);
+    }
+#endif
+#if LNW_PROBE_DISTURB == 16
+    if (ph == rank) {
+      const size_t t = (size_t)blockIdx.x * PA_THREADS + threadIdx.x;
+      mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd, hh1, nullptr, probe_layers + t * 48,
+                    probe_split + t * 12, probe_pre + t * 16);
+    }
+#elif LNW_PROBE_DISTURB == 15
+    if (ph == rank) {
+      f32x4v *ls = probe_layers + ((size_t)blockIdx.x * PA_THREADS + threadIdx.x) * 48;
+      mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd, hh1, nullptr, ls);
+    }
+#elif LNW_PROBE_DISTURB == 14
+    if (ph == rank) {
+      // the MLP's fc1 operands as it loaded them from the tile, against the saved
+      // rows (stage 2); its head outputs (hh) kept for the rerun below
+      f32x4v xs[4 * Q1];
+      mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd, hh1, xs);
+      bool bad = false;
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++) {
+        const long long grow = r0 + (threadIdx.x & ~(WAVE - 1)) + rt * 16 + m;
+        if (grow >= PROBE_ROWS) continue;
+        const float *b = probe_buf + (size_t)grow * PROBE_W;
+#pragma unroll
+        for (int q = 0; q < Q1; q++)
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            bad = bad || __float_as_uint(xs[rt * Q1 + q][j]) != __float_as_uint(b[16 * q + 4 * g + j]);
+      }
+      if (bad) atomicAdd(&probe_cnt[2 * 64 + lane], 1u);
+    }
+#else
     if (ph == rank) mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
-#if LNW_PROBE_DISTURB == 10  // the partner redoes its head (same tile)
-    else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
+#endif
+#if LNW_PROBE_DISTURB == 10 || LNW_PROBE_DISTURB >= 13  // the partner redoes its head (same tile)
+    else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows, LNW_PROBE_DISTURB >= 13);
 #elif LNW_PROBE_DISTURB == 12  // ... comparing every stage
     else head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows, 1);
 #else  // the partner's work (tools/build_probes.sh)
@@ -709,6 +847,82 @@ __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *
 #endif
     __syncthreads();
   }
+#if LNW_PROBE_DISTURB == 16
+  {  // stages: 0/1 split terms (rt 0-2 / rt 3), 2/3 fc1 before tanh, 4/5 h1 after tanh
+    float m2[NOUT], l2[NOUT];
+    f32x4v hh2[4], l2s[48], pre2[16];
+    bf16x8 sp2[12];
+    mlp_heads<Q1>(pa, Fw, warea, lane, g, m, m2, l2, hh2, nullptr, l2s, sp2, pre2);
+    const size_t t = (size_t)blockIdx.x * PA_THREADS + threadIdx.x;
+    const bf16x8 *sp = probe_split + t * 12;
+    const f32x4v *pr = probe_pre + t * 16, *ls = probe_layers + t * 48;
+    bool bad[3][2] = {{false, false}, {false, false}, {false, false}};
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) {
+#pragma unroll
+      for (int k = 0; k < 3; k++)
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+          bad[0][rt == 3] = bad[0][rt == 3] || __builtin_bit_cast(unsigned short, sp[3 * rt + k][j]) !=
+                                                   __builtin_bit_cast(unsigned short, sp2[3 * rt + k][j]);
+#pragma unroll
+      for (int nt = 0; nt < 4; nt++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          bad[1][rt == 3] = bad[1][rt == 3] || __float_as_uint(pr[rt * 4 + nt][j]) != __float_as_uint(pre2[rt * 4 + nt][j]);
+          bad[2][rt == 3] = bad[2][rt == 3] || __float_as_uint(ls[rt * 4 + nt][j]) != __float_as_uint(l2s[rt * 4 + nt][j]);
+        }
+    }
+#pragma unroll
+    for (int L = 0; L < 3; L++)
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+        if (bad[L][u]) atomicAdd(&probe_cnt[(2 * L + u) * 64 + lane], 1u);
+  }
+#elif LNW_PROBE_DISTURB == 15
+  {  // per layer (h1, h2, h3, heads) and row tile: stage 2 L + (rt == 3), L = layer
+    float m2[NOUT], l2[NOUT];
+    f32x4v hh2[4], l2s[48];
+    mlp_heads<Q1>(pa, Fw, warea, lane, g, m, m2, l2, hh2, nullptr, l2s);
+    const f32x4v *ls = probe_layers + ((size_t)blockIdx.x * PA_THREADS + threadIdx.x) * 48;
+    bool bad[4][2] = {{false, false}, {false, false}, {false, false}, {false, false}};
+#pragma unroll
+    for (int L = 0; L < 3; L++)
+#pragma unroll
+      for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+        for (int nt = 0; nt < (L == 2 ? 2 : 4); nt++)
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            bad[L][rt == 3] = bad[L][rt == 3] ||
+                              __float_as_uint(ls[(L * 4 + rt) * 4 + nt][j]) != __float_as_uint(l2s[(L * 4 + rt) * 4 + nt][j]);
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) bad[3][rt == 3] = bad[3][rt == 3] || __float_as_uint(hh2[rt][j]) != __float_as_uint(hh1[rt][j]);
+#pragma unroll
+    for (int L = 0; L < 4; L++)
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+        if (bad[L][t]) atomicAdd(&probe_cnt[(2 * L + t) * 64 + lane], 1u);
+  }
+#elif LNW_PROBE_DISTURB == 14
+  {  // stage 3: the final per-row outputs, stage 4: the head outputs before the gather
+    float m2[NOUT], l2[NOUT];
+    f32x4v hh2[4];
+    mlp_heads<Q1>(pa, Fw, warea, lane, g, m, m2, l2, hh2);
+    bool bo = false, bh = false;
+#pragma unroll
+    for (int v = 0; v < NOUT; v++)
+      bo = bo || __float_as_uint(m2[v]) != __float_as_uint(mean[v]) || __float_as_uint(l2[v]) != __float_as_uint(lsd[v]);
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) bh = bh || __float_as_uint(hh2[rt][j]) != __float_as_uint(hh1[rt][j]);
+    if (bo) atomicAdd(&probe_cnt[3 * 64 + lane], 1u);
+    if (bh) atomicAdd(&probe_cnt[4 * 64 + lane], 1u);
+  }
+#endif
 #endif
 }
 
@@ -1092,11 +1306,11 @@ int lnw_policy_act(const lnw_policy_args *args, void *stream) {
   return hipGetLastError() == hipSuccess ? 0 : LNW_EDEVICE;
 }
 
-#if defined(LNW_PROBE_DISTURB) && LNW_PROBE_DISTURB == 12
-// probe 12's counters [stage][lane] since the last call (then zeroed)
+#if defined(LNW_PROBE_DISTURB) && (LNW_PROBE_DISTURB >= 12)
+// probe 12's / 13's counters [stage][lane] since the last call (then zeroed)
 int lnw_probe_counts(unsigned *host) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(probe_cnt), sizeof(probe_cnt)) != hipSuccess) return LNW_EDEVICE;
-  static const unsigned zero[5 * 64] = {};
+  static const unsigned zero[PROBE_STAGES * 64] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(probe_cnt), zero, sizeof(zero)) == hipSuccess ? 0 : LNW_EDEVICE;
 }
 #endif

@@ -12,7 +12,7 @@ mkdir -p tools/probe
 
 wait
 # the partner wave's work while a wave runs its MLP (LNW_PROBE_DISTURB modes)
-for d in 1 2 3 4 5 6 7 8 9 10 11 12; do
+for d in 1 2 3 4 5 6 7 8 9 10 11 12 13 14 15 16; do
   /opt/rocm/bin/hipcc $F -DLNW_PROBE_DISTURB=$d $C/lnw_actor.hip -o tools/probe/actor_disturb$d.so &
 done
 wait

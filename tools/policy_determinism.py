@@ -115,10 +115,26 @@ def main():
                               float((x - y).abs().max()), "rows", sorted(set(rr.tolist()))[:6],
                               "waves", sorted(set((rr // 64).tolist()))[:6], flush=True)
         if hasattr(L, "lnw_probe_counts"):  # probe 12: rows whose second head differed, per stage
-            cnt = (C.c_uint * 320)()
+            cnt = (C.c_uint * 640)()
             L.lnw_probe_counts(cnt)
-            for st, name in enumerate(["window loads", "pooled conv1 maps (LDS)", "conv head out",
-                                       "LayerNorm tail loads", "LayerNorm out"]):
+            names = (["fc1 bf16 split terms, row tiles 0-2", "fc1 bf16 split terms, row tile 3",
+                      "fc1 before tanh, row tiles 0-2", "fc1 before tanh, row tile 3",
+                      "h1 after tanh, row tiles 0-2", "h1 after tanh, row tile 3", "-", "-", "-", "-"]
+                     if "disturb16" in (path or "") else
+                     [f"layer {lay} ({'heads' if lay == 'h4' else 'tanh'}) in row tiles {t} vs the rerun"
+                      for lay in ("h1", "h2", "h3", "h4") for t in ("0-2", "3")]
+                     if "disturb15" in (path or "") else
+                     ["tile read back after the second head's write (beside the partner's MLP)",
+                      "tile row just before the wave's own MLP",
+                      "fc1 operands as the MLP loaded them from the tile",
+                      "per-row outputs vs a rerun of the MLP (MLPs beside MLPs)",
+                      "head outputs before the lane gather vs the rerun"]
+                     if ("disturb13" in (path or "") or "disturb14" in (path or "")) else
+                     ["window loads", "pooled conv1 maps (LDS)", "conv head out", "LayerNorm tail loads",
+                      "LayerNorm out"])
+            for st, name in enumerate(names):
+                if name == "-":
+                    continue
                 c = list(cnt[st * 64:(st + 1) * 64])
                 if sum(c):
                     ln = [l for l in range(64) if c[l]]
