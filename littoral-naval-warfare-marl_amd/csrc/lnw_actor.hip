@@ -364,6 +364,14 @@ __device__ __forceinline__ void mfma_layer3(const bf16x8 *__restrict__ F, const 
     bf16x8 b0[4], b1[4], b2[4];
 #pragma unroll
     for (int rt = 0; rt < 4; rt++) split3(xb[rt][2 * p], xb[rt][2 * p + 1], b0[rt], b1[rt], b2[rt]);
+#ifdef LNW_MLP_SPLIT_FENCE
+    // probe: every split term computed (materialised in its registers) before
+    // the first MFMA of the pair is issued: no vector instruction of this block
+    // co-executing with its MFMAs
+#pragma unroll
+    for (int rt = 0; rt < 4; rt++) asm volatile("" : "+v"(b0[rt]), "+v"(b1[rt]), "+v"(b2[rt]));
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if (split_save && p == 0) {  // (diagnostics probe 16)
 #pragma unroll
       for (int rt = 0; rt < 4; rt++) {
@@ -764,7 +772,9 @@ __device__ __forceinline__ void head_and_mlp(const PolicyArgs &pa, const float *
   constexpr int Q1 = NI / 16;
   head_to_tile<NI>(pa, P, warea, lane, valid, e, i, istride, r0, rows);
 #ifndef LNW_PROBE_DISTURB
+#ifndef LNW_POLICY_OVERLAP  // (probe builds: each wave's MLP right after its own head)
   if constexpr (PA_THREADS > WAVE) __syncthreads();  // every head done before any MLP
+#endif
   mlp_heads<Q1>(pa, Fw, warea, lane, g, m, mean, lsd);
 #else
   constexpr int NWB = PA_THREADS / WAVE;
