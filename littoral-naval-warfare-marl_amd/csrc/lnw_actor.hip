@@ -201,6 +201,22 @@ __device__ __forceinline__ void load_tail(const float *x, int D, float (&tl)[NT]
   for (int k = 0; k < NT; k++) tl[k] = x[WIN + k < D ? WIN + k : D - 1];
 }
 
+// The same for a 16-B aligned row of D % 4 == 0 floats (lnw_policy_act checks
+// both): the float4 quads from x[48] on, one dwordx4 per quad instead of one
+// dword load per value (quad indices clamped into the row; the values past
+// n_in - 12 they duplicate are unused)
+template <int NT>
+__device__ __forceinline__ void load_tail_q(const float *x, int D, float (&tl)[NT]) {
+  constexpr int NQ = (NT + 1 + 3) / 4;  // x[48] .. x[48 + NT]
+  const int D4 = D >> 2;
+  const f32x4 *x4 = (const f32x4 *)x;
+  f32x4 q[NQ];
+#pragma unroll
+  for (int j = 0; j < NQ; j++) q[j] = x4[12 + j < D4 ? 12 + j : D4 - 1];
+#pragma unroll
+  for (int k = 0; k < NT; k++) tl[k] = q[(k + 1) >> 2][(k + 1) & 3];
+}
+
 // (the torch implementation's conv head, off the fused path: one wave per
 // SIMD, so the compiler has the registers to keep the head out of scratch)
 template <int NI>
@@ -605,7 +621,11 @@ __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *
     }
     // the tail after the head (its registers are the head's), one batch of loads
     float tl[NI - 12];
+#ifdef LNW_POLICY_SCALAR_TAIL  // (probe builds: the per-value loads, A/B)
     load_tail(a.obs + e * istride + (long long)i * D, D, tl);
+#else
+    load_tail_q(a.obs + e * istride + (long long)i * D, D, tl);
+#endif
     PROBE_STAGE(3, 106, tl);
     layer_norm_tail<NI>(P, tl, n_in, h, u);
     PROBE_STAGE(4, 170, u);
