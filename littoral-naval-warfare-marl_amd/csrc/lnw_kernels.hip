@@ -3087,6 +3087,12 @@ __device__ __forceinline__ void step_body(
       if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
     }
   }
+#ifdef LNW_PROBE_QUIET_ONLY
+  // timing probe (tools/gpu): the templated kernels without phase S / O code, so
+  // the quiet path's registers are allocated without phase S live; loud
+  // workgroups then do nothing (wrong results)
+  if constexpr (ST && NW > 1) return;
+#endif
   // The contact variant's phase S splits by side (templated 4v4, loud
   // workgroups; step_kernel PS): wave 0 plays blue's turns and wave 1 red's, and
   // the rows are written after it (phase O) instead of emitted by wave 1 during
@@ -4189,6 +4195,25 @@ void prof_report(lnw_handle *h, hipStream_t st, int nwg) {
       if (r[14] && r[12] > r[8] && r[8]) { rq += (double)(r[12] - r[8]); nr2++; }
     }
     if (nr2) fprintf(stderr, "[lnw prof] repeated quiet test (diagnostics): %.2f us\n", rq / nr2 * us);
+  }
+  {  // quiet small workgroups (direct mode): each wave's phase-Q work from the
+     // test's end (slots 27 / 15), wave 1's rows staged (28) and stored (5)
+     // from the barrier (9)
+    double q0 = 0, q1 = 0, rb = 0, rc = 0;
+    int nd = 0;
+    for (int w = 0; w < nwg; w++) {
+      const unsigned long long *r = &t[(size_t)w * PROF_SLOTS];
+      if (!r[14] || !r[28] || !r[15] || !r[27] || r[28] < r[9]) continue;
+      nd++;
+      q0 += (double)(r[27] - r[8]);
+      q1 += (double)(r[15] - r[8]);
+      rb += (double)(r[28] - r[9]);
+      rc += (double)(r[5] - r[28]);
+    }
+    if (nd)
+      fprintf(stderr, "[lnw prof] quiet direct %d: phase-Q work wave 0 %.2f, wave 1 %.2f us; after the barrier "
+                      "rows staged %.2f, stored %.2f us\n",
+              nd, q0 / nd * us, q1 / nd * us, rb / nd * us, rc / nd * us);
   }
   if (nq)
     fprintf(stderr, "[lnw prof] quiet workgroups %d: M %.2f us, A*+barrier %.2f us, quiet test %.2f us, Q+barrier %.2f us; "
