@@ -3066,7 +3066,12 @@ __device__ __forceinline__ void step_body(
         __syncthreads();
       }
       if (wid == 0) prof_stamp(S, 7);
-      bool wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
+      // small workgroups (epw * NB <= 64): the test spread over (ship, env) lanes
+      bool wq;
+      if (NB == NR && UN == 1 && P.epw * NB <= WAVE && !(P.dbg_skip & 268435456))  // (bit 28: per-env test)
+        wq = wg_quiet_spread_t<NB, NB>(P, c, lane, r2col);
+      else
+        wq = __all(env_quiet_t<NB, NR>(P, c, lane, r2col[lane]));
       if (wid == 0) prof_stamp(S, 8);
 #ifdef LNW_DIAG
       if (P.dbg_skip & (1 << 24)) {  // diagnostics: the quiet test again, its code now cached
