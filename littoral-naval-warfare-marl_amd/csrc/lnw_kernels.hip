@@ -3015,6 +3015,19 @@ __device__ __forceinline__ void step_body(
   const bool pre = ST && NW == 2 && dt == LNW_ACT_F32 && !(P.dbg_skip & 4) && !(P.dbg_skip & 8388608);
   f32x4 vpre[MAXPRE];
   if (pre) preload_rows_f32<NW, MAXPRE>(actions, env0, nenv, A, wid, vpre);
+  // small quiet-capable workgroups (quiet_step_t's direct mode, epw * NB <= 64):
+  // wave 0's env counters and draw counter loaded at launch, their HBM round
+  // trip inside phase L's instead of between phase Q and the tail (nothing
+  // before the tail writes them; LNW_DEBUG_SKIP bit 29: loaded in phase Q)
+  int evp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  Rng rngp{};
+  const bool evpre = ST && NW == 2 && UN == 1 && NB == NR && epw * NB <= WAVE && P.los_mode == 0 &&
+                     !(P.dbg_skip & (1 << 29));
+  if (evpre && wid == 0 && valid) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) evp[q] = S.envi[q * E + env];
+    rngp = make_rng(P, S, env);
+  }
   if (wid == 0) {
     prof_stamp(S, 0);
     // XCC id (hwreg 20, bits 3:0) and HW_ID (hwreg 4: CU, SH, SE) of this workgroup
@@ -3086,7 +3099,7 @@ __device__ __forceinline__ void step_body(
                                          env0, valid);
         else
           quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
-                               rew_r, done_out, cog_out, env0, nenv, valid);
+                               rew_r, done_out, cog_out, env0, nenv, valid, evpre, evp, rngp);
         return;
       }
       if (UN > 1) __syncthreads();  // a loud unit: the barrier the quiet units pass after phase Q
@@ -4275,10 +4288,11 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   // the shipped library honours only the knobs that change the launch shape or
   // code path, never the results (bit 9: no quiet path, 15: the group kernel's
   // fire loop entry by entry, 17: per-lane bearing loop, 22/23: where the
-  // head's loads are issued); section skips and
+  // head's loads are issued, 28: the per-env quiet test in small workgroups,
+  // 29: their env counters loaded in phase Q); section skips and
   // replaced arithmetic exist only in the diagnostics build (-DLNW_DIAG,
   // lnw.build.build_diag)
-  constexpr int kResultPreserving = 512 | 32768 | 131072 | 4194304 | 8388608;
+  constexpr int kResultPreserving = 512 | 32768 | 131072 | 4194304 | 8388608 | (1 << 28) | (1 << 29);
   if (h->dbg_skip & ~kResultPreserving) {
     const int bad = h->dbg_skip & ~kResultPreserving;
     delete h;
