@@ -3021,7 +3021,9 @@ __device__ __forceinline__ void step_body(
   // before the tail writes them; LNW_DEBUG_SKIP bit 29: loaded in phase Q)
   int evp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   Rng rngp{};
-  const bool evpre = ST && NW == 2 && UN == 1 && NB == NR && epw * NB <= WAVE && P.los_mode == 0 &&
+  // (not in the contact variants: their registers run out in phase S, and these
+  // live ranges put 52 B per lane of scratch into them — melee 2.3 us slower)
+  const bool evpre = ST && !CW && NW == 2 && UN == 1 && NB == NR && epw * NB <= WAVE && P.los_mode == 0 &&
                      !(P.dbg_skip & (1 << 29));
   if (evpre && wid == 0 && valid) {
 #pragma unroll
