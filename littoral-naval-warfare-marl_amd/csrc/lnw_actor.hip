@@ -619,12 +619,19 @@ __device__ __forceinline__ void head_to_tile(const PolicyArgs &pa, const float *
       PROBE_STAGE(2, 94, h);
 #endif
     }
-    // the tail after the head (its registers are the head's), one batch of loads
+    // the tail after the head (its registers are the head's), one batch of loads;
+    // the row's address again from an opaque copy of the row index, so no 64-bit
+    // address lives across the head (where the register file is full: it went
+    // to scratch, and the kernel with it)
     float tl[NI - 12];
+    int r_t = (int)(r0 + (threadIdx.x & ~(WAVE - 1)) + lane);
+    asm volatile("" : "+v"(r_t));
+    const int e_t = r_t / n, i_t = r_t - e_t * n;
+    const float *xt = a.obs + (long long)e_t * istride + (long long)i_t * D;
 #ifdef LNW_POLICY_SCALAR_TAIL  // (probe builds: the per-value loads, A/B)
-    load_tail(a.obs + e * istride + (long long)i * D, D, tl);
+    load_tail(xt, D, tl);
 #else
-    load_tail_q(a.obs + e * istride + (long long)i * D, D, tl);
+    load_tail_q(xt, D, tl);
 #endif
     PROBE_STAGE(3, 106, tl);
     layer_norm_tail<NI>(P, tl, n_in, h, u);
