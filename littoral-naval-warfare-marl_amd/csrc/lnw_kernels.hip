@@ -3094,7 +3094,7 @@ __device__ __forceinline__ void step_body(
         if (wid == 0) prof_stamp(S, 12);
       }
 #endif
-      if (wq) {
+      if (__builtin_expect(wq, 1)) {  // (quiet path laid out as the fall-through)
         if constexpr (UN > 1)
           quiet_step_units_t<NB, NR, UN>(P, S, c, lds_dyn, L, lstride, unit, lane, env, wid, duct_all,
                                          ushare, actions, obs_b, obs_r, rew_b, rew_r, done_out, cog_out,
