@@ -56,6 +56,7 @@ struct KParams {
   int no_obs;         // lnw_step without observation outputs (both pointers NULL)
   long long obs_stride[2];  // lnw_observe_ex: floats between envs' rows per side (0: packed)
   int dbg_skip;       // diagnostics only (LNW_DEBUG_SKIP): bit0 obs, bit1 phase S, bit2 phase M, bit7 get_obs in S, bit8 reward, bit9 no quiet path, bit10 no window reads in quiet emission, bit11 no phase-S LOS prefetch, bit12 device atan2 instead of the bearing table, bit13 4-ship phase-S rows stored row by row instead of line-aligned, bit15 the group kernel's fire loop entry by entry
+  int qdirect;        // (last: the tail padding; the fields above keep their kernarg offsets) quiet workgroups stage whole 64-row side blocks (qbig) and wave 1 writes every row itself, in slabs of 64 / nb envs (step_qdirect)
 };
 
 // Device state (SoA, agent-major [field][agent][env] so a wave of envs reads

@@ -2964,7 +2964,7 @@ extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
 // observation passes go through one workgroup-wide queue that every free wave
 // of a quiet unit serves, so the CU's units finish their stream together
 // instead of 4-5 us apart (the spread of separate workgroups on one CU).
-template <int NB, int NR, bool CW, bool REFW, int UN, bool PS>
+template <int NB, int NR, bool CW, bool REFW, int UN, bool PS, bool SL>
 __device__ __forceinline__ void step_body(
     const KParams &P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
@@ -2984,7 +2984,11 @@ __device__ __forceinline__ void step_body(
   const int nb = ST ? NB : P.nb, nr = ST ? NR : P.nr;
   const int A = nb + nr;
   // small quiet workgroups get whole-side row stages (quiet_step_t's direct mode)
-  const int qbig_rows = ST && NB == NR && EPW == WAVE && P.los_mode == 0 && epw * NB <= WAVE ? epw * NB : 0;
+  // (the host's rows, step_launch_lds_bytes: one slab below 64 / NB envs, two in
+  // the SL instantiation; the one-slab kernels keep their own test of epw)
+  const int qbig_rows = !(ST && NB == NR && EPW == WAVE && P.los_mode == 0) ? 0
+                        : SL ? (P.qdirect ? WAVE : 0)
+                             : (epw * NB <= WAVE ? epw * NB : 0);
   LdsLayout L = lds_layout(A, nb, nr, S.nmax, P.G * P.W16, P.G, qbig_rows);
   const int lstride = (L.total + 15) & ~15;  // one LDS block per unit
   Cols c = carve(lds_dyn + unit * lstride, L);
@@ -3100,7 +3104,7 @@ __device__ __forceinline__ void step_body(
                                          ushare, actions, obs_b, obs_r, rew_b, rew_r, done_out, cog_out,
                                          env0, valid);
         else
-          quiet_step_t<NB, NR>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
+          quiet_step_t<NB, NR, SL>(P, S, c, lane, env, wid, duct_col, &qclaim, actions, obs_b, obs_r, rew_b,
                                rew_r, done_out, cog_out, env0, nenv, valid, evpre, evp, rngp);
         return;
       }
@@ -3508,11 +3512,13 @@ __device__ __forceinline__ void step_body(
 }
 
 // One step of every env (lnw_step; lnw_step_seq makes one launch per step)
-template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false>
+// SL: quiet workgroups of up to 128 / NB envs write their rows in two slabs
+// (step_qdirect; a separate instantiation, so the one-slab kernels keep their code)
+template <int NB, int NR, bool CW = false, bool REFW = false, int UN = 1, bool PS = false, bool SL = false>
 __global__ __launch_bounds__(NB > 0 && EPW == WAVE ? 2 * WAVE * UN : WAVE, NB > 0 ? 2 : 1) void step_kernel(
     KParams P, KState S, void *actions, const uint8_t *row_kind, float *obs_b, float *obs_r,
     float *rew_b, float *rew_r, int32_t *done_out, float *cog_out) {
-  step_body<NB, NR, CW, REFW, UN, PS>(P, S, actions, row_kind, obs_b, obs_r, rew_b, rew_r, done_out, cog_out);
+  step_body<NB, NR, CW, REFW, UN, PS, SL>(P, S, actions, row_kind, obs_b, obs_r, rew_b, rew_r, done_out, cog_out);
 }
 
 #include "lnw_group.inc"
@@ -3941,6 +3947,7 @@ struct lnw_handle {
   // diagnostics knobs, read once at lnw_create (LNW_DEBUG_SKIP / LNW_PROF / LNW_FORCE_GENERIC)
   int dbg_skip = 0;
   bool prof = false, force_generic = false, no_group = false, group_fits = false, no_units = false;
+  bool no_slab = false;  // LNW_NO_SLAB: no two-slab direct rows (A/B)
   bool force_group = false;  // LNW_FORCE_GROUP (A/B): the group kernel for templated team sizes too
   bool no_split_rows = false;  // LNW_NO_SPLIT_ROWS (A/B): row-writing contact steps keep phase S on one wave
   bool store_wt = false;
@@ -3999,10 +4006,38 @@ size_t step_lds_bytes(const lnw_handle *h) {
 
 // the step launch's LDS: step_lds_bytes plus the whole-side row stages of
 // small quiet workgroups (the same condition step_kernel evaluates)
-size_t step_launch_lds_bytes(const lnw_handle *h, int epw) {
+// compute units of the handle's device (cached per device)
+int device_ncu(int dev) {
+  static int cache[64] = {0};
+  int &c = cache[dev & 63];
+  if (c == 0) {
+    int n = 0;
+    c = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return c;
+}
+
+// Quiet workgroups' direct rows (quiet_step_t): a workgroup of up to 64 / nb envs
+// stages both sides' rows whole (qbig) and wave 1 builds and stores every row
+// from registers; up to 128 / nb envs it does so in two slabs of 64 / nb envs,
+// for the non-contact kernels and only when the larger LDS still holds the whole
+// grid at once (config 3 at N = 4: 16 384 envs, 32 per workgroup). Larger
+// workgroups stream their rows in staged passes (quiet_emit_t).
+bool step_qdirect(const lnw_handle *h, int epw) {
   const bool tmpl = !h->force_generic && !h->has_medium && h->params.los_mode == 0 && h->nb == h->nr &&
                     h->nb >= 2 && h->nb <= 4 && EPW == WAVE;
-  const int rows = tmpl && epw * h->nb <= WAVE ? epw * h->nb : 0;
+  if (!tmpl) return false;
+  if (epw * h->nb <= WAVE) return true;
+  // (4v4 only: step_kernel<4, 4, .., SL> is the one two-slab instantiation)
+  if (h->nb != 4 || h->contact || h->no_slab || epw * h->nb > 2 * WAVE) return false;
+  const LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G, WAVE);
+  int per_cu = (int)((160 * 1024) / ((size_t)L.total + 1024));
+  if (per_cu > 4) per_cu = 4;  // 256 VGPRs: two waves per SIMD
+  return (h->E + epw - 1) / epw <= (long long)device_ncu(h->device) * per_cu;
+}
+
+size_t step_launch_lds_bytes(const lnw_handle *h, int epw) {
+  const int rows = step_qdirect(h, epw) ? (epw * h->nb < WAVE ? epw * h->nb : WAVE) : 0;
   LdsLayout L = lds_layout(h->A, h->nb, h->nr, h->nmax, h->G * h->W16, h->G, rows);
   return (size_t)L.total;
 }
@@ -4310,6 +4345,7 @@ int lnw_create(const lnw_params *params, int32_t n_envs, int32_t nb, int32_t nr,
   h->no_split_rows = getenv("LNW_NO_SPLIT_ROWS") != nullptr;
   // LNW_NO_UNITS: one 64-env unit per workgroup for the headline shape (A/B tests)
   h->no_units = getenv("LNW_NO_UNITS") != nullptr;
+  h->no_slab = getenv("LNW_NO_SLAB") != nullptr;
   h->kp.xcd_remap = getenv("LNW_NO_XCD_REMAP") == nullptr ? 1 : 0;
   // LNW_GROUP_MARCH=1: the group kernel marches its pair LOS over the LDS
   // terrain mask instead of loading LOS-table words (A/B)
@@ -4495,6 +4531,8 @@ int lnw_load_terrain(lnw_handle *h, const uint8_t *grid_host, int32_t G) {
     const size_t uneed = (size_t)UNITS * ((step_lds_bytes(h) + 15) & ~(size_t)15);
     h->units_fit = uneed <= (size_t)UNITS_LDS_MAX;
     if (!(lds_opt_in & dbit) && (need > 64 * 1024 || gneed > 64 * 1024 || uneed > 64 * 1024)) {
+      HIPCHK(hipFuncSetAttribute((const void *)step_kernel<4, 4, false, false, 1, false, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, GROUP_LDS_MAX));
       const void *ks[17] = {(const void *)step_kernel<4, 4, true, false, 1, true>,
                             (const void *)step_kernel<0, 0>,       (const void *)step_kernel<2, 2>,
                             (const void *)step_kernel<3, 3>,       (const void *)step_kernel<4, 4>,
@@ -4615,6 +4653,7 @@ int step_launch(lnw_handle *h, void *actions_dev, int32_t action_dtype,
   k.dbg_skip = h->dbg_skip;
   k.store_wt = h->store_wt;
   KState s = make_state(h);
+  k.qdirect = step_qdirect(h, k.epw) ? 1 : 0;
   size_t lds = step_launch_lds_bytes(h, k.epw);
   dim3 grid((h->E + k.epw - 1) / k.epw), block(WAVE);
   hipStream_t st = (hipStream_t)stream;
@@ -4664,6 +4703,9 @@ int step_launch(lnw_handle *h, void *actions_dev, int32_t action_dtype,
       step_kernel<4, 4, true, false, 1, true><<<grid, dim3(2 * WAVE), lds, st>>>(
           k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
     else if (cw) LNW_STEP(4, 4, true, false);
+    else if (k.qdirect && k.epw * 4 > WAVE)  // two-slab direct rows (step_qdirect)
+      step_kernel<4, 4, false, false, 1, false, true><<<grid, dim3(2 * WAVE), lds, st>>>(
+          k, s, actions_dev, row_kind_dev, obs_blue_dev, obs_red_dev, rew_blue_dev, rew_red_dev, done_dev, cog_dev);
     else LNW_STEP(4, 4, false, false);
   }
   else if (templated && h->nb == 3) { if (cw) LNW_STEP(3, 3, true, false); else LNW_STEP(3, 3, false, false); }

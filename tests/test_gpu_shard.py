@@ -1,7 +1,8 @@
 """The metric's real per-GPU path at N = 8 and config 2: 8 192 and 4 096 4v4 envs
 on one GPU take the small-workgroup quiet direct mode (16 envs per workgroup,
 quiet_step_t in csrc/lnw_quiet.inc, DESIGN.md "Direct mode for small
-workgroups"). Checked directly against the CPU oracle (orc_fullsize_range,
+workgroups"); 16 384 envs (config 3's shard at N = 4) take it with 32 envs per
+workgroup, the rows written in two slabs of 16 envs. Checked directly against the CPU oracle (orc_fullsize_range,
 oracle/lnw_oracle.c) with the default envs-per-workgroup choice:
 
 * "reference": every env at the reference spawns (game.py:560-585), the
@@ -42,7 +43,7 @@ def _melee(grid, n, seed):
 
 @pytest.mark.parametrize("trained_red", [True, False])
 @pytest.mark.parametrize("layout", ["reference", "mixed"])
-@pytest.mark.parametrize("E", [8192, 4096])
+@pytest.mark.parametrize("E", [8192, 4096, 16384])
 def test_shard_quiet_direct_vs_oracle(E, layout, trained_red):
     from lnw import _abi
     from lnw.batched import BatchedGame
@@ -55,7 +56,9 @@ def test_shard_quiet_direct_vs_oracle(E, layout, trained_red):
         pos[blocks] = _melee(grid, len(blocks), seed=E)
     sc = Scenario(landing_ops=False, auto_reset=True, episode_steps=40, trained_red=trained_red)
     g = BatchedGame(E, ["small"] * 4, ["large"] * 4, scenario=sc, grid=grid, seed=seed)
-    assert g.epw == 16, "the default choice at these sizes is the quiet direct mode's 16 envs per workgroup"
+    # the default choice: 16 envs per workgroup at 8 192 / 4 096 (one slab), 32 at
+    # 16 384 (config 3 at N = 4: wave 1 writes the rows in two slabs of 16 envs)
+    assert g.epw == (32 if E == 16384 else 16)
     g.reset(positions=REF_SPAWNS, pos_per_env=torch.from_numpy(pos))
     acts = np.random.default_rng(31 + trained_red).random((S, E, 8, 4), dtype=np.float32)
     mult = _mult(2 * 4 * 68, seed=13)

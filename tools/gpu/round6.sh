@@ -261,8 +261,33 @@ quiet_likely)
   L=littoral-naval-warfare-marl_amd/lnw/liblnw.so
   bash tools/gpu/ab_lib.sh 3 tools/probe/liblnw_prev.so $L "" "--global-envs 8192" "--global-envs 4096" || exit $?
   ;;
+scale_shapes)
+  # round 6: the per-GPU shapes of N = 2 and N = 4 (32 768 and 16 384 envs) timed,
+  # with their LNW_PROF timelines
+  bash tools/gpu/timeline.sh sh32768 "--global-envs 32768" 2>&1 | grep -E "wg=|quiet|grid:|sh32768" || exit 1
+  bash tools/gpu/timeline.sh sh16384 "--global-envs 16384" 2>&1 | grep -E "wg=|quiet|grid:|sh16384" || exit 1
+  ;;
+epw_shapes)
+  # round 6: envs per workgroup at the N = 2 / 4 per-GPU shapes (LNW_EPW_RT
+  # overrides choose_epw): 16384 and 32768 envs at 16 / 32 / 64 envs per workgroup
+  for a in "16384 16" "16384 32" "32768 16" "32768 32" "32768 64"; do
+    set -- $a
+    LNW_EPW_RT=$2 timeout -k 10 120 python bench.py --no-secondary --no-cpu-baseline --steps 200 --warmup 20 \
+      --global-envs $1 > gpurun_out/epw.json 2>gpurun_out/epw.err || { tail -5 gpurun_out/epw.err; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/epw.json')); print('envs $1 epw $2', round(d['roofline']['kernel_ms_mean']*1e3, 2), 'us')"
+  done
+  ;;
+slab_rows)
+  # round 6: quiet workgroups of 32 envs write their rows in two 16-env slabs
+  # (step_qdirect) against the previous build and the LNW_NO_SLAB knob, then the
+  # shard / parity / full-size / units / state tests
+  L=littoral-naval-warfare-marl_amd/lnw/liblnw.so
+  bash tools/gpu/ab_lib.sh 3 tools/probe/liblnw_prev.so $L "--global-envs 16384" "--global-envs 8192" "--global-envs 4096" "" || exit $?
+  LNW_LIB=$PWD/$L bash tools/gpu/ab_env.sh LNW_NO_SLAB 2 "--global-envs 16384" || exit $?
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_units.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_state.py -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/tk.log 2>&1; rc=$?; tail -3 gpurun_out/tk.log; exit $rc
+  ;;
 *)
-  echo "usage: bash tools/gpu/round6.sh {crash_race|race_nowait|race_nowait_nt|policy_probe14|policy_probe15_16|policy_probe16_c4fetch|policy_fence|policy_tail_quads|c4_rows_batched|shard_timelines|quiet_columns_upfront|quiet_pairs_packed|quiet_only_probe|quiet_test_spread|counters_at_launch|counters_knob|evidence_first_a|evidence_first_b|sincos_probe|sincos_certified|move_cell_fast|store_wt_knob|no_phase_q_barrier|counters_removed|counters_noncontact|policy_tail_address|final_evidence_a|final_evidence_b|critic_prefetch|final_stress|quiet_likely}"
+  echo "usage: bash tools/gpu/round6.sh {slab_rows|scale_shapes|epw_shapes|crash_race|race_nowait|race_nowait_nt|policy_probe14|policy_probe15_16|policy_probe16_c4fetch|policy_fence|policy_tail_quads|c4_rows_batched|shard_timelines|quiet_columns_upfront|quiet_pairs_packed|quiet_only_probe|quiet_test_spread|counters_at_launch|counters_knob|evidence_first_a|evidence_first_b|sincos_probe|sincos_certified|move_cell_fast|store_wt_knob|no_phase_q_barrier|counters_removed|counters_noncontact|policy_tail_address|final_evidence_a|final_evidence_b|critic_prefetch|final_stress|quiet_likely}"
   exit 2
   ;;
 esac
