@@ -451,6 +451,10 @@ def secondary_lines(args):
     K, W = args.secondary_steps, min(args.warmup, 20)
     out = {}
     for name, E, sp, lm, mm, desc in (
+            ("config3_shard_32768", 32768, "reference", 0, 0,
+             "config 3's per-GPU shard at N=2: 32 768 4v4 envs, reference spawns"),
+            ("config3_shard_16384", 16384, "reference", 0, 0,
+             "config 3's per-GPU shard at N=4: 16 384 4v4 envs, reference spawns"),
             ("config3_shard_8192", 8192, "reference", 0, 0,
              "config 3's per-GPU shard at N=8: 8 192 4v4 envs, reference spawns"),
             ("config2_4096", 4096, "reference", 0, 0, "config 2: 4 096 4v4 envs, reference spawns"),
