@@ -288,7 +288,8 @@ slab_rows)
   ;;
 units2)
   # round 6: two-unit workgroups (LNW_UNITS2) at the N = 2 and N = 4 per-GPU shapes,
-  # interleaved A/B of the knob; the units / shard tests with it on
+  # interleaved A/B of the knob; the units / shard tests with it on (the knob and
+  # its kernel were removed after this measured slower: DESIGN.md)
   bash tools/gpu/ab_env.sh LNW_UNITS2 3 "--global-envs 32768" "--global-envs 16384" || exit $?
   LNW_UNITS2=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_shard.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tk.log 2>&1; rc=$?; tail -3 gpurun_out/tk.log; exit $rc
   ;;
