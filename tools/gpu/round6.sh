@@ -293,8 +293,21 @@ units2)
   bash tools/gpu/ab_env.sh LNW_UNITS2 3 "--global-envs 32768" "--global-envs 16384" || exit $?
   LNW_UNITS2=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_shard.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/tk.log 2>&1; rc=$?; tail -3 gpurun_out/tk.log; exit $rc
   ;;
+epw8)
+  # round 6: 8 envs per workgroup at config 2 (4 096 envs: 512 workgroups instead of
+  # 256 of 16) and at 8 192, interleaved with the default choice
+  for r in 1 2 3; do
+    for a in "4096 0" "4096 8" "8192 0" "8192 8"; do
+      set -- $a
+      if [ "$2" = 0 ]; then unset LNW_EPW_RT; else export LNW_EPW_RT=$2; fi
+      timeout -k 10 120 python bench.py --no-secondary --no-cpu-baseline --steps 200 --warmup 20 \
+        --global-envs $1 > gpurun_out/epw.json 2>gpurun_out/epw.err || { tail -5 gpurun_out/epw.err; exit 1; }
+      python -c "import json; d=json.load(open('gpurun_out/epw.json')); print('r$r envs $1 epw ${2/#0/default}', round(d['roofline']['kernel_ms_mean']*1e3, 2), 'us')"
+    done
+  done
+  ;;
 *)
-  echo "usage: bash tools/gpu/round6.sh {units2|slab_rows|scale_shapes|epw_shapes|crash_race|race_nowait|race_nowait_nt|policy_probe14|policy_probe15_16|policy_probe16_c4fetch|policy_fence|policy_tail_quads|c4_rows_batched|shard_timelines|quiet_columns_upfront|quiet_pairs_packed|quiet_only_probe|quiet_test_spread|counters_at_launch|counters_knob|evidence_first_a|evidence_first_b|sincos_probe|sincos_certified|move_cell_fast|store_wt_knob|no_phase_q_barrier|counters_removed|counters_noncontact|policy_tail_address|final_evidence_a|final_evidence_b|critic_prefetch|final_stress|quiet_likely}"
+  echo "usage: bash tools/gpu/round6.sh {epw8|units2|slab_rows|scale_shapes|epw_shapes|crash_race|race_nowait|race_nowait_nt|policy_probe14|policy_probe15_16|policy_probe16_c4fetch|policy_fence|policy_tail_quads|c4_rows_batched|shard_timelines|quiet_columns_upfront|quiet_pairs_packed|quiet_only_probe|quiet_test_spread|counters_at_launch|counters_knob|evidence_first_a|evidence_first_b|sincos_probe|sincos_certified|move_cell_fast|store_wt_knob|no_phase_q_barrier|counters_removed|counters_noncontact|policy_tail_address|final_evidence_a|final_evidence_b|critic_prefetch|final_stress|quiet_likely}"
   exit 2
   ;;
 esac
