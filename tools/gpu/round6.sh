@@ -306,8 +306,15 @@ epw8)
     done
   done
   ;;
+loud_call)
+  # round 6: the units kernel's loud units behind a call (step_loud_unit) against
+  # the previous build, headline and shard shapes, then the units / parity tests
+  L=littoral-naval-warfare-marl_amd/lnw/liblnw.so
+  bash tools/gpu/ab_lib.sh 3 tools/probe/liblnw_prev.so $L "" "--global-envs 8192" "--global-envs 16384" "--spawns melee" || exit $?
+  timeout -k 10 900 python -u -m pytest tests/test_gpu_units.py tests/test_gpu_shard.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_state.py -m gpu -x -q --timeout 600 --timeout-method thread > gpurun_out/tk.log 2>&1; rc=$?; tail -3 gpurun_out/tk.log; exit $rc
+  ;;
 *)
-  echo "usage: bash tools/gpu/round6.sh {epw8|units2|slab_rows|scale_shapes|epw_shapes|crash_race|race_nowait|race_nowait_nt|policy_probe14|policy_probe15_16|policy_probe16_c4fetch|policy_fence|policy_tail_quads|c4_rows_batched|shard_timelines|quiet_columns_upfront|quiet_pairs_packed|quiet_only_probe|quiet_test_spread|counters_at_launch|counters_knob|evidence_first_a|evidence_first_b|sincos_probe|sincos_certified|move_cell_fast|store_wt_knob|no_phase_q_barrier|counters_removed|counters_noncontact|policy_tail_address|final_evidence_a|final_evidence_b|critic_prefetch|final_stress|quiet_likely}"
+  echo "usage: bash tools/gpu/round6.sh {loud_call|epw8|units2|slab_rows|scale_shapes|epw_shapes|crash_race|race_nowait|race_nowait_nt|policy_probe14|policy_probe15_16|policy_probe16_c4fetch|policy_fence|policy_tail_quads|c4_rows_batched|shard_timelines|quiet_columns_upfront|quiet_pairs_packed|quiet_only_probe|quiet_test_spread|counters_at_launch|counters_knob|evidence_first_a|evidence_first_b|sincos_probe|sincos_certified|move_cell_fast|store_wt_knob|no_phase_q_barrier|counters_removed|counters_noncontact|policy_tail_address|final_evidence_a|final_evidence_b|critic_prefetch|final_stress|quiet_likely}"
   exit 2
   ;;
 esac
